@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X feature engine.
+
+metric (BASELINE.json): candidates/sec of the 8-feature (Lyon) path on synthetic 128-bin
+profile + 128-bin DM rows, plus HBM GB/s vs peak.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS_PER_GPU] [--path lyon8|bates22]
+
+One "step" = one pass of the hot path (pfe_lyon8_u8 through the C-ABI, device pointers,
+inputs resident in HBM) over the rank's whole batch of synthetic candidates (config 2:
+10M rows per GPU).  For N > 1 the driver starts one process per GPU with
+torch.distributed.run; candidates shard with no data-path collective (weak scaling:
+10M rows per rank); the timed region is bracketed by barrier + synchronize and the MAX over
+ranks is reported; value = all rows processed by all ranks / that time.
+
+Besides the contract fields the JSON line carries:
+  roofline     : the lyon8 kernel's algorithmic bytes per launch (n * (lp + ld + 64) B)
+                 / its average duration, measured with HIP events on the stream the kernel
+                 runs on, against the 8.0 TB/s HBM3E peak; traffic = PMC-measured HBM bytes
+                 per launch from profiles/ when a matching summary is committed, else null
+  cpu_baseline : the reference-equivalent per-candidate numpy/scipy loop (oracle.lyon.lyon8,
+                 the scalar port of PHCXFile.py:320-379) timed on this host, 1 core, on a
+                 bounded sample of the same synthetic rows (rank 0, N=1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=10_000_000, help="candidates per GPU")
+    ap.add_argument("--lp", type=int, default=128)
+    ap.add_argument("--ld", type=int, default=128)
+    ap.add_argument("--path", choices=["lyon8", "bates22"], default="lyon8")
+    ap.add_argument("--cpu-sample", type=int, default=8000,
+                    help="rows for the CPU baseline sample (0 disables)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def load_traffic(name: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/*.json)."""
+    p = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline_lyon8(lp, ld, sample):
+    import numpy as np
+
+    from oracle.lyon import lyon8
+    from pulsarfeatureextractor_amd.synth import lyon_batch
+
+    prof, dm = lyon_batch(sample, lp, ld, seed=4242)
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        lyon8(prof[:50], dm[:50])  # warm imports
+        t0 = time.perf_counter()
+        lyon8(prof, dm)
+        dt = time.perf_counter() - t0
+    return {
+        "value": sample / dt,
+        "unit": "candidates/sec",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{sample} synthetic {lp}-bin profile + {ld}-bin DM rows through the "
+                  f"reference-equivalent per-candidate numpy.mean/std + scipy.stats.skew/"
+                  f"kurtosis loop (oracle.lyon.lyon8), {dt:.1f} s on 1 host core",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist_on = world > 1
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from pulsarfeatureextractor_amd._native import Engine
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    eng = Engine(local)
+    stream = torch.cuda.Stream(device=local)  # the kernel's stream; events record on it
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+
+    n = args.n
+    if args.path != "lyon8":
+        raise SystemExit("bench.py: only the lyon8 headline path is benchmarked in this round")
+    # rank-specific synthetic shard, resident in HBM before timing
+    prof, dm = lyon_batch_torch(n, args.lp, args.ld, seed=20261017 + rank, device=f"cuda:{local}")
+    out = torch.empty((n, 8), dtype=torch.float64, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def step():
+        eng.lyon8(prof, dm, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel-duration events on the kernel's own stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    if dist_on:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    total_rows = n * world * args.steps
+    value = total_rows / elapsed
+    bytes_per_launch = n * (args.lp + args.ld + 8 * 8)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(f"lyon8_u8_{args.lp}x{args.ld}_n{n}_pmc.json")
+
+    result = {
+        "metric": "candidates/sec (8-feature path, 128-bin)",
+        "value": value,
+        "unit": "candidates/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8->int64/f64",
+        "data": "synthetic (SURVEY.md §8(d) recipe, generated on device)",
+        "config": {
+            "workload": f"config 2: {n} synthetic candidates per GPU, {args.lp}-bin profile + "
+                        f"{args.ld}-bin DM, 8 Lyon moment features (pfe_lyon8_u8)",
+            "candidates_per_gpu": n,
+            "profile_bins": args.lp,
+            "dm_bins": args.ld,
+            "parallelism": f"candidate shards x{world}, no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "pfe::lyon8_u8_fast<128>",
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_kernel_ms": kern_ms,
+            "avg_kernel_ms_max_over_ranks": kern_ms_max,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
+        result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+/*
+ * pfe.h — C-ABI of libpfe.so, the MI355X (gfx950) batched pulsar-candidate feature engine.
+ *
+ * This is the drop-in boundary for the per-candidate score path of
+ * scienceguyrob/PulsarFeatureExtractor (ScoreGenerator.py).  The reference computes one
+ * candidate at a time in Python; every entry point here is the BATCHED equivalent of one
+ * reference interface, taking row-major candidate arrays (plain pointers + sizes, no
+ * framework types) and writing one row of fp64 scores per candidate.
+ *
+ * Interfaces replaced (reference paths relative to PulsarFeatureExtractor/src/):
+ *   pfe_lyon8_u8   <- PHCXFile.computeProfileStatScores          PHCXFile.py:320-349
+ *                     + PHCXFile.computeDMCurveStatScores         PHCXFile.py:351-379
+ *                     (concatenated as in DataProcessor.dmprof    DataProcessor.py:884-886;
+ *                      SUPERBPHCXFile.py has identical bodies at the same lines)
+ *   pfe_lyon8_f64  <- the same two functions on float profiles (PFDFile.py:522-583)
+ *   pfe_bates22    <- PHCXFile.compute                            PHCXFile.py:383-409
+ *                     (score groups 1-4 :413, 5-11 :475, 12-15 :547, 16-19 :589, 20-22 :633)
+ *
+ * Conventions
+ *   - One handle per (device, stream).  Calls on one handle are serialised by the caller;
+ *     different handles may be used concurrently from different threads.
+ *   - Caller owns all input/output buffers.  With PFE_FLAG_DEVICE_PTRS the pointers are
+ *     device (HBM) pointers and the call is asynchronous on the handle's stream (no host
+ *     sync); without it they are host pointers and the library stages them through
+ *     per-handle device scratch, returning when the outputs are back on the host.
+ *   - Raw IEEE values are returned (NaN/inf included).  NaN/inf -> "0" replacement is the
+ *     writer's job, as in DataProcessor.storeScore (DataProcessor.py:321-325).
+ *   - Return value: 0 = OK, otherwise a PFE_E* code; the text is in pfe_last_error().
+ *   - There is NO CPU backend: pfe_create(-1, ...) fails.  The CPU restatement used for
+ *     parity testing lives in oracle/ and is not part of this library.
+ */
+#ifndef PFE_H_
+#define PFE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFE_ABI_VERSION 1
+
+/* return codes */
+#define PFE_OK 0
+#define PFE_EINVAL 1   /* bad argument (null pointer, negative size, unsupported layout) */
+#define PFE_EDEVICE 2  /* HIP runtime failure (allocation, launch, copy) */
+#define PFE_ENODEV 3   /* no such device / no GPU present */
+
+/* flags */
+#define PFE_FLAG_DEVICE_PTRS 0x1u /* all array arguments are device pointers */
+
+/* Per-candidate status bits (pfe_bates22).  A non-zero status means the reference would
+ * have raised inside Candidate.calculateScores and DataProcessor would have logged the
+ * candidate to CandidateErrorLog.txt and dropped its row (DataProcessor.py:517-523). */
+#define PFE_ST_SINE_FAIL      0x001u /* scores 1-4 raised            (PHCXFile.py:467-470) */
+#define PFE_ST_GAUSS_FAIL     0x002u /* scores 5-11 raised           (PHCXFile.py:540-543) */
+#define PFE_ST_DMFIT_FAIL     0x004u /* scores 16-19 raised          (PHCXFile.py:626-629) */
+#define PFE_ST_SUBBAND_FAIL   0x008u /* scores 20-22 raised          (PHCXFile.py:665-668) */
+#define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
+                                        s10=s11=1e6 (ProfileOperations.py:762-764) */
+#define PFE_ST_FAIL_MASK      0x0FFu
+
+typedef struct pfe_handle pfe_handle;
+
+/* Query the ABI version compiled into the library. */
+int pfe_abi_version(void);
+
+/* Number of visible GPUs (0 when none); never fails. */
+int pfe_device_count(void);
+
+/* Create a handle bound to GPU `device` (>= 0) and its own non-blocking stream. */
+int pfe_create(int device, pfe_handle** out);
+void pfe_destroy(pfe_handle* h);
+
+/* Text of the last error on this handle (or of the last failed pfe_create when h is NULL). */
+const char* pfe_last_error(const pfe_handle* h);
+
+/* Replace the handle's stream (e.g. torch.cuda.current_stream().cuda_stream).  NULL restores
+ * the handle's own stream.  The library never destroys a stream it did not create. */
+int pfe_set_stream(pfe_handle* h, void* hip_stream);
+/* Block until all work queued on the handle's stream has finished. */
+int pfe_synchronize(pfe_handle* h);
+
+/* ---------------------------------------------------------------------------------------
+ * 8 Lyon features.
+ *   prof : n rows of lp uint8 bins (PHCX 02X-decoded profile), row r at prof + r*prof_stride
+ *   dm   : n rows of ld uint8 values (PHCX DataBlock of section 0), row r at dm + r*dm_stride
+ *   out  : n x 8 fp64, row-major, per candidate
+ *          [prof_mean, prof_std, prof_skew, prof_kurt, dm_mean, dm_std, dm_skew, dm_kurt]
+ *          std is ddof=0; skew is the biased g1 and kurt the biased Fisher g2 of
+ *          scipy.stats; both are NaN when the row has zero variance (scipy >= 1.9).
+ *   status : may be NULL; set to 0 for every row (the 8-feature path has no failure mode).
+ * Requires lp >= 1, ld >= 1, strides >= row lengths.
+ * --------------------------------------------------------------------------------------- */
+int pfe_lyon8_u8(pfe_handle* h, const uint8_t* prof, int64_t prof_stride, int32_t lp,
+                 const uint8_t* dm, int64_t dm_stride, int32_t ld, int64_t n, double* out,
+                 uint32_t* status, uint32_t flags);
+
+/* Same with fp64 rows (PFD profiles are float; PFDFile.py:522-583).  Two-pass fp64
+ * moments, as numpy/scipy compute them. */
+int pfe_lyon8_f64(pfe_handle* h, const double* prof, int64_t prof_stride, int32_t lp,
+                  const double* dm, int64_t dm_stride, int32_t ld, int64_t n, double* out,
+                  uint32_t* status, uint32_t flags);
+
+/* ---------------------------------------------------------------------------------------
+ * 22 Bates scores (PHCX / SUPERB PHCX).
+ *   prof    : n x lp uint8 profile (Profile of the scored section)
+ *   sub     : n x nsub x lsb uint8 sub-bands (SubBands of the scored section)
+ *   dmcurve : n x ndm fp64 reduced DM curve (PHCXOperations.dm_curve of that section's
+ *             DataBlock: max over the first 127 of every 128 values), abscissa
+ *             x_k = 128*(k+1) - 129 + 128 = 128k - 1 ... see scal
+ *   scal    : n x PFE_NSCAL fp64 per-candidate scalars (layout below)
+ *   out     : n x 22 fp64 in reference score order (score 1 in column 0)
+ *   status  : n x uint32 PFE_ST_* bits (required)
+ * Strides are in elements and equal the row length (dense rows).
+ * --------------------------------------------------------------------------------------- */
+#define PFE_NSCAL 8
+#define PFE_SCAL_PERIOD_MS 0 /* BaryPeriod * 1000            (PHCXOperations.py:109) */
+#define PFE_SCAL_SNR 1       /* Snr                            (:107) */
+#define PFE_SCAL_DM 2        /* Dm                             (:108) */
+#define PFE_SCAL_WIDTH 3     /* Width                          (:110) */
+#define PFE_SCAL_DM_START 4  /* float(DmIndex token[1])        (:172-182) */
+#define PFE_SCAL_DM_END 5    /* float(DmIndex last token)      (:182) */
+#define PFE_SCAL_LENGTH_ALL 6 /* len(decoded DataBlock)        (:168) */
+#define PFE_SCAL_RESERVED 7
+
+typedef struct pfe_bates_in {
+  const uint8_t* prof;  /* n x lp */
+  int32_t lp;
+  const uint8_t* sub;   /* n x nsub x lsb */
+  int32_t nsub;
+  int32_t lsb;
+  const double* dmcurve; /* n x ndm */
+  int32_t ndm;
+  const double* scal;   /* n x PFE_NSCAL */
+  int64_t n;
+} pfe_bates_in;
+
+int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PFE_H_ */

@@ -1,0 +1,272 @@
+"""ctypes binding of libpfe.so (the C-ABI declared in include/pfe.h).
+
+This is the reference-side binding a maintainer would add to PulsarFeatureExtractor: a thin
+ctypes layer over the extern "C" entry points.  It never falls back to a CPU
+implementation: if the library is missing or no GPU is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PFE_LIBRARY", os.path.join(_HERE, "lib", "libpfe.so"))
+
+PFE_OK = 0
+PFE_FLAG_DEVICE_PTRS = 0x1
+PFE_NSCAL = 8
+PFE_ST_FAIL_MASK = 0x0FF
+PFE_ST_SINE_FAIL = 0x001
+PFE_ST_GAUSS_FAIL = 0x002
+PFE_ST_DMFIT_FAIL = 0x004
+PFE_ST_SUBBAND_FAIL = 0x008
+PFE_ST_DGF_INDEXERROR = 0x100
+
+# every symbol include/pfe.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED_SYMBOLS = (
+    "pfe_abi_version",
+    "pfe_device_count",
+    "pfe_create",
+    "pfe_destroy",
+    "pfe_last_error",
+    "pfe_set_stream",
+    "pfe_synchronize",
+    "pfe_lyon8_u8",
+    "pfe_lyon8_f64",
+    "pfe_bates22",
+)
+
+
+class PfeError(RuntimeError):
+    """Raised when a libpfe call fails (the message is pfe_last_error())."""
+
+
+class BatesIn(C.Structure):
+    _fields_ = [
+        ("prof", C.c_void_p),
+        ("lp", C.c_int32),
+        ("sub", C.c_void_p),
+        ("nsub", C.c_int32),
+        ("lsb", C.c_int32),
+        ("dmcurve", C.c_void_p),
+        ("ndm", C.c_int32),
+        ("scal", C.c_void_p),
+        ("n", C.c_int64),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _preload_torch_hip_runtime():
+    """Share ONE HIP runtime with PyTorch.
+
+    torch ships its own libamdhip64.so (soname libamdhip64.so.7).  If libpfe.so resolved
+    /opt/rocm's copy first, the process would hold two HIP runtimes and whichever initialises
+    second sees no GPU.  Loading torch's copy globally first makes libpfe's NEEDED entry bind
+    to it, and torch later recognises the same file (same inode) -- without importing torch.
+    """
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    for loc in spec.submodule_search_locations:
+        p = os.path.join(loc, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            return C.CDLL(p, mode=C.RTLD_GLOBAL)
+    return None
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load libpfe.so and declare its signatures.  Raises OSError when it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise OSError(
+                f"libpfe.so not found at {p}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback)"
+            )
+        if os.environ.get("PFE_SYSTEM_HIP", "0") != "1":
+            _preload_torch_hip_runtime()
+        lib = C.CDLL(p)
+        vp, i32, i64, u32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32
+        lib.pfe_abi_version.restype = C.c_int
+        lib.pfe_abi_version.argtypes = []
+        lib.pfe_device_count.restype = C.c_int
+        lib.pfe_device_count.argtypes = []
+        lib.pfe_create.restype = C.c_int
+        lib.pfe_create.argtypes = [C.c_int, C.POINTER(vp)]
+        lib.pfe_destroy.restype = None
+        lib.pfe_destroy.argtypes = [vp]
+        lib.pfe_last_error.restype = C.c_char_p
+        lib.pfe_last_error.argtypes = [vp]
+        lib.pfe_set_stream.restype = C.c_int
+        lib.pfe_set_stream.argtypes = [vp, vp]
+        lib.pfe_synchronize.restype = C.c_int
+        lib.pfe_synchronize.argtypes = [vp]
+        lib.pfe_lyon8_u8.restype = C.c_int
+        lib.pfe_lyon8_u8.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
+        lib.pfe_lyon8_f64.restype = C.c_int
+        lib.pfe_lyon8_f64.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
+        lib.pfe_bates22.restype = C.c_int
+        lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _ptr(a) -> int:
+    """Raw address of a numpy array or a torch tensor (host or device)."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch.Tensor
+
+
+def _is_device(a) -> bool:
+    if isinstance(a, np.ndarray):
+        return False
+    return bool(getattr(a, "is_cuda", False))
+
+
+class Engine:
+    """One libpfe handle: a GPU ordinal plus a HIP stream.
+
+    Arguments may be numpy arrays (host; the call stages and synchronises) or torch CUDA
+    tensors (device; the call is asynchronous on the engine's stream).  Mixed placements
+    are rejected.
+    """
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.pfe_create(int(device), C.byref(h))
+        if rc != PFE_OK:
+            raise PfeError(self.lib.pfe_last_error(None).decode())
+        self._h = h
+        self.device = device
+
+    # -- lifecycle -----------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.pfe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != PFE_OK:
+            raise PfeError(self.lib.pfe_last_error(self._h).decode())
+
+    def set_stream(self, stream_handle: int | None):
+        """Launch on an external hipStream_t (e.g. a torch.cuda.Stream's ``cuda_stream``).
+
+        None restores the engine's own stream.  The HIP null stream (handle 0, torch's
+        default stream) cannot be selected: use an explicit stream."""
+        if stream_handle == 0:
+            raise ValueError("set_stream: the null stream (0) cannot be selected; "
+                             "use a torch.cuda.Stream()")
+        self._check(self.lib.pfe_set_stream(self._h, stream_handle))
+
+    def synchronize(self):
+        self._check(self.lib.pfe_synchronize(self._h))
+
+    # -- 8 Lyon features -----------------------------------------------------------------
+    def lyon8(self, prof, dm, out=None, status=None):
+        """[mean,std,skew,kurt] of each profile row then each DM row -> (n, 8) float64."""
+        if prof.ndim != 2 or dm.ndim != 2 or prof.shape[0] != dm.shape[0]:
+            raise ValueError("prof and dm must be 2-D with the same number of rows")
+        n = prof.shape[0]
+        dev = _is_device(prof)
+        if dev != _is_device(dm):
+            raise ValueError("prof and dm must both be host arrays or both device tensors")
+        if dev:
+            import torch
+
+            if out is None:
+                out = torch.empty((n, 8), dtype=torch.float64, device=prof.device)
+            dtype_ok = {torch.uint8: "u8", torch.float64: "f64"}
+            kind = dtype_ok.get(prof.dtype)
+            if kind is None or dm.dtype != prof.dtype:
+                raise TypeError("lyon8: rows must be uint8 or float64 (same dtype)")
+            ps, ds = prof.stride(0), dm.stride(0)
+            if prof.stride(1) != 1 or dm.stride(1) != 1 or not out.is_contiguous():
+                raise ValueError("lyon8: rows must be contiguous")
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            if out is None:
+                out = np.empty((n, 8), dtype=np.float64)
+            if prof.dtype == np.uint8 and dm.dtype == np.uint8:
+                kind = "u8"
+            elif prof.dtype == np.float64 and dm.dtype == np.float64:
+                kind = "f64"
+            else:
+                raise TypeError("lyon8: rows must be uint8 or float64 (same dtype)")
+            prof = prof if prof.strides[1] == prof.itemsize else np.ascontiguousarray(prof)
+            dm = dm if dm.strides[1] == dm.itemsize else np.ascontiguousarray(dm)
+            ps, ds = prof.strides[0] // prof.itemsize, dm.strides[0] // dm.itemsize
+            if out.dtype != np.float64 or not out.flags.c_contiguous or out.shape != (n, 8):
+                raise ValueError("lyon8: out must be a contiguous (n, 8) float64 array")
+            flags = 0
+        fn = self.lib.pfe_lyon8_u8 if kind == "u8" else self.lib.pfe_lyon8_f64
+        st = None if status is None else _ptr(status)
+        self._check(
+            fn(self._h, _ptr(prof), ps, prof.shape[1], _ptr(dm), ds, dm.shape[1], n,
+               _ptr(out), st, flags)
+        )
+        return out
+
+    # -- 22 Bates scores -----------------------------------------------------------------
+    def bates22(self, prof, sub, dmcurve, scal, out=None, status=None):
+        """22 scores per candidate -> ((n, 22) float64, (n,) uint32 status)."""
+        n = prof.shape[0]
+        if sub.shape[0] != n or dmcurve.shape[0] != n or scal.shape[0] != n:
+            raise ValueError("bates22: inputs must have the same number of rows")
+        if sub.ndim != 3 or scal.shape[1] != PFE_NSCAL:
+            raise ValueError("bates22: sub must be (n,nsub,lsb), scal (n,%d)" % PFE_NSCAL)
+        dev = _is_device(prof)
+        if dev:
+            import torch
+
+            if out is None:
+                out = torch.empty((n, 22), dtype=torch.float64, device=prof.device)
+            if status is None:
+                status = torch.empty((n,), dtype=torch.int32, device=prof.device)
+            for t in (prof, sub, dmcurve, scal, out, status):
+                if not t.is_contiguous():
+                    raise ValueError("bates22: device tensors must be contiguous")
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            prof = np.ascontiguousarray(prof, dtype=np.uint8)
+            sub = np.ascontiguousarray(sub, dtype=np.uint8)
+            dmcurve = np.ascontiguousarray(dmcurve, dtype=np.float64)
+            scal = np.ascontiguousarray(scal, dtype=np.float64)
+            if out is None:
+                out = np.empty((n, 22), dtype=np.float64)
+            if status is None:
+                status = np.empty((n,), dtype=np.uint32)
+            flags = 0
+        bi = BatesIn(
+            _ptr(prof), prof.shape[1], _ptr(sub), sub.shape[1], sub.shape[2],
+            _ptr(dmcurve), dmcurve.shape[1], _ptr(scal), n,
+        )
+        self._check(self.lib.pfe_bates22(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
+        return out, status

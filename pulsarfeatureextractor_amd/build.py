@@ -1,0 +1,83 @@
+"""Build libpfe.so (all HIP kernels + the C-ABI) in-tree for gfx950.
+
+The shared library lands in ``pulsarfeatureextractor_amd/lib/libpfe.so`` so that it travels
+with the repository snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+BUILDDIR = os.path.join(HERE, "lib", "obj")
+LIB = os.path.join(LIBDIR, "libpfe.so")
+SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip"]
+ARCH = os.environ.get("PFE_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+COMMON = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    # Keep every fp64 operation individually rounded, as numpy evaluates it: no FMA
+    # contraction and no fast-math in any kernel (parity with the reference's arithmetic).
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def _needs(obj: str, deps: list[str]) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILDDIR, exist_ok=True)
+    cc = hipcc()
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "pfe.h"))
+    objs = []
+    jobs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILDDIR, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or _needs(o, [s] + headers):
+            jobs.append([cc, *COMMON, "-c", s, "-o", o])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    if force or jobs or not os.path.exists(LIB):
+        tmp = LIB + ".tmp"
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

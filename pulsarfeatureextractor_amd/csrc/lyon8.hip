@@ -1,0 +1,330 @@
+// lyon8.hip — the 8 Lyon statistical-moment features on gfx950.
+//
+// Reference: PHCXFile.computeProfileStatScores / computeDMCurveStatScores
+// (PulsarFeatureExtractor/src/PHCXFile.py:320-379) compute, per candidate,
+//     [mean(bins), std(bins), skew(bins), kurtosis(bins)]
+// of the integrated profile and of the DM array, with numpy (mean: sum/n; std: ddof=0)
+// and scipy.stats (biased skew g1 = m3/m2^1.5, biased Fisher kurtosis g2 = m4/m2^2 - 3,
+// NaN when m2 <= (eps*mean)^2).  The dmprof driver concatenates profile then DM
+// (DataProcessor.py:884-886).
+//
+// Design (HBM-bound streaming reduction, no MFMA):
+//   * PHCX bins are 02X bytes, so all power sums are EXACT integers.  We form
+//     y = x - 128 (a byte XOR), and accumulate T1..T4 = sum y^k with the gfx950 packed
+//     integer dot instructions (v_dot4_i32_i8 for y and y^2, v_dot2_{i32_i16,u32_u16} for
+//     y^3 and y^4 on packed 16-bit squares).  ~3.3 VALU ops per input byte.
+//   * The exact central-moment numerators n^k*m_k come from T1..T4 in 64-bit modular
+//     integer arithmetic (exact for n <= 430; a 128-bit variant covers long DM arrays),
+//     so each m_k is correctly rounded from its exact rational value: mean and std match
+//     numpy bit-for-bit whenever numpy's own sums are exact (n a power of two <= 256),
+//     skew/kurt to a few ulp.
+//   * Fast path (lp == ld == L in {64,128,256}, 16-B aligned rows): L/32 lanes per
+//     candidate, each lane streams 32 B of the profile row and 32 B of the DM row with
+//     dwordx4 loads; the group reduces with DPP quad/half-row butterflies; each lane then
+//     finalises 8/(L/32) of the candidate's 8 outputs and stores them as one contiguous
+//     16/32/8-byte vector, so a wave writes a dense 1 KiB span of the output matrix.
+//   * Generic path (any lengths/alignment): one wave per (candidate,row), byte loads,
+//     64-bit per-lane sums, 128-bit finalisation.
+
+#include "pfe_common.h"
+
+namespace pfe {
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+struct RowSums {
+  int t1;        // sum y        (|.| <= 128*L)
+  int t2;        // sum y^2      (<= 16384*L)
+  int t3;        // sum y^3      (|.| <= 2^21*L)
+  uint64_t t4;   // sum y^4      (<= 2^28*L)
+};
+
+// Accumulate 4 bytes packed in x into the row sums.  t4a is a 32-bit partial for y^4
+// (<= 2^29 added per call); callers flush it to 64 bits every 2 calls.
+__device__ __forceinline__ void acc_dword(uint32_t x, int& t1, int& t2, int& t3, uint32_t& t4a) {
+  const uint32_t v = x ^ 0x80808080u;  // bytes are now two's-complement y = x-128
+  t1 = __builtin_amdgcn_sdot4((int)v, 0x01010101, t1, false);
+  t2 = __builtin_amdgcn_sdot4((int)v, (int)v, t2, false);
+  // zero-extend bytes {0,2} and {1,3} into 16-bit halves
+  const uint32_t lo = x & 0x00FF00FFu;
+  const uint32_t hi = (x >> 8) & 0x00FF00FFu;
+  short2v ylo = __builtin_bit_cast(short2v, lo) - (short2v){128, 128};
+  short2v yhi = __builtin_bit_cast(short2v, hi) - (short2v){128, 128};
+  ushort2v qlo = __builtin_bit_cast(ushort2v, ylo) * __builtin_bit_cast(ushort2v, ylo);  // y^2 <= 16384
+  ushort2v qhi = __builtin_bit_cast(ushort2v, yhi) * __builtin_bit_cast(ushort2v, yhi);
+  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qlo), ylo, t3, false);
+  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qhi), yhi, t3, false);
+  t4a = __builtin_amdgcn_udot2(qlo, qlo, t4a, false);
+  t4a = __builtin_amdgcn_udot2(qhi, qhi, t4a, false);
+}
+
+__device__ __forceinline__ void acc_uint4(const u32x4 q, RowSums& s) {
+  uint32_t a = 0, b = 0;
+  acc_dword(q.x, s.t1, s.t2, s.t3, a);
+  acc_dword(q.y, s.t1, s.t2, s.t3, a);
+  acc_dword(q.z, s.t1, s.t2, s.t3, b);
+  acc_dword(q.w, s.t1, s.t2, s.t3, b);
+  s.t4 += (uint64_t)a + (uint64_t)b;
+}
+
+// Exact central-moment numerators from shifted power sums (y = x - 128):
+//   N2 = n^2 m2 = n T2 - T1^2
+//   N3 = n^3 m3 = n^2 T3 - 3 n T1 T2 + 2 T1^3
+//   N4 = n^4 m4 = n^3 T4 - 4 n^2 T1 T3 + 6 n T1^2 T2 - 3 T1^4
+// Evaluated modulo 2^64; every true value is < 2^63 for n <= 430, so the result is exact.
+struct Moments {
+  double mean, m2, m3, m4;
+};
+
+__device__ __forceinline__ Moments moments_i64(long long n, long long T1, long long T2,
+                                               long long T3, unsigned long long T4) {
+  typedef unsigned long long u64;
+  const u64 un = (u64)n, t1 = (u64)T1, t2 = (u64)T2, t3 = (u64)T3;
+  const u64 n2 = un * un, n3 = n2 * un;
+  const u64 t1s = t1 * t1;
+  const long long N2 = (long long)(un * t2 - t1s);
+  const long long N3 = (long long)(n2 * t3 - 3ull * un * t1 * t2 + 2ull * t1s * t1);
+  const u64 N4 = n3 * T4 - 4ull * n2 * t1 * t3 + 6ull * un * t1s * t2 - 3ull * t1s * t1s;
+  const double dn = (double)n;
+  Moments m;
+  m.mean = (double)(T1 + 128ll * n) / dn;
+  m.m2 = (double)N2 / (dn * dn);
+  m.m3 = (double)N3 / (dn * dn * dn);
+  m.m4 = (double)N4 / ((dn * dn) * (dn * dn));
+  return m;
+}
+
+// 128-bit variant for long rows (PHCX DataBlock: nDM*128 values).  Requires n < 2^24.
+__device__ __forceinline__ double i128_to_f64(__int128 v) {
+  const bool neg = v < 0;
+  unsigned __int128 u = neg ? (unsigned __int128)(-v) : (unsigned __int128)v;
+  const uint64_t hi = (uint64_t)(u >> 64), lo = (uint64_t)u;
+  // hi*2^64 + lo with a single final rounding when hi < 2^53 (always true here)
+  double r = (double)hi * 18446744073709551616.0 + (double)lo;
+  return neg ? -r : r;
+}
+
+__device__ __forceinline__ Moments moments_i128(long long n, long long T1, long long T2,
+                                                long long T3, unsigned long long T4) {
+  typedef __int128 i128;
+  const i128 in = n, t1 = T1, t2 = T2, t3 = T3, t4 = (i128)T4;
+  const i128 n2 = in * in, n3 = n2 * in;
+  const i128 t1s = t1 * t1;
+  const i128 N2 = in * t2 - t1s;
+  const i128 N3 = n2 * t3 - 3 * in * t1 * t2 + 2 * t1s * t1;
+  const i128 N4 = n3 * t4 - 4 * n2 * t1 * t3 + 6 * in * t1s * t2 - 3 * t1s * t1s;
+  const double dn = (double)n;
+  Moments m;
+  m.mean = (double)(T1 + 128ll * n) / dn;
+  m.m2 = i128_to_f64(N2) / (dn * dn);
+  m.m3 = i128_to_f64(N3) / (dn * dn * dn);
+  m.m4 = i128_to_f64(N4) / ((dn * dn) * (dn * dn));
+  return m;
+}
+
+// scipy.stats.skew / kurtosis (bias=True, Fisher) zero-variance rule:
+//   zero = m2 <= (eps * mean)^2  ->  NaN
+__device__ __forceinline__ bool zero_var(const Moments& m) {
+  const double e = 2.220446049250313e-16 * m.mean;
+  return m.m2 <= e * e;
+}
+
+__device__ __forceinline__ double stat_k(const Moments& m, int k) {
+  // k: 0 mean, 1 std, 2 skew, 3 kurt
+  if (k == 0) return m.mean;
+  if (k == 1) return sqrt(m.m2);
+  if (zero_var(m)) return __builtin_nan("");
+  if (k == 2) return m.m3 / (m.m2 * sqrt(m.m2));
+  return m.m4 / (m.m2 * m.m2) - 3.0;
+}
+
+// ---- fast path -------------------------------------------------------------------------
+// L in {64,128,256}; LPC = L/32 lanes per candidate; each lane: 32 B of each row.
+template <int L>
+__global__ __launch_bounds__(256) void lyon8_u8_fast(const uint8_t* __restrict__ prof,
+                                                     int64_t ps,
+                                                     const uint8_t* __restrict__ dm,
+                                                     int64_t ds, int64_t n,
+                                                     double* __restrict__ out) {
+  constexpr int LPC = L / 32;       // lanes per candidate: 2, 4, 8
+  constexpr int CPW = 64 / LPC;     // candidates per wave step
+  constexpr int SPL = 8 / LPC;      // outputs per lane: 4, 2, 1
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPC;
+  const int cw = lane / LPC;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+
+  for (int64_t base = wave * CPW; base < n; base += nwaves * CPW) {
+    const int64_t c = base + cw;
+    const bool valid = c < n;
+    u32x4 p0 = {0, 0, 0, 0}, p1 = p0, d0 = p0, d1 = p0;
+    if (valid) {
+      const u32x4* pp = reinterpret_cast<const u32x4*>(prof + c * ps + sub * 32);
+      const u32x4* dp = reinterpret_cast<const u32x4*>(dm + c * ds + sub * 32);
+      p0 = __builtin_nontemporal_load(pp);
+      p1 = __builtin_nontemporal_load(pp + 1);
+      d0 = __builtin_nontemporal_load(dp);
+      d1 = __builtin_nontemporal_load(dp + 1);
+    }
+    RowSums sp = {0, 0, 0, 0}, sd = {0, 0, 0, 0};
+    acc_uint4(p0, sp);
+    acc_uint4(p1, sp);
+    acc_uint4(d0, sd);
+    acc_uint4(d1, sd);
+    sp.t1 = group_sum_i32<LPC>(sp.t1);
+    sp.t2 = group_sum_i32<LPC>(sp.t2);
+    sp.t3 = group_sum_i32<LPC>(sp.t3);
+    sp.t4 = group_sum_u64<LPC>(sp.t4);
+    sd.t1 = group_sum_i32<LPC>(sd.t1);
+    sd.t2 = group_sum_i32<LPC>(sd.t2);
+    sd.t3 = group_sum_i32<LPC>(sd.t3);
+    sd.t4 = group_sum_u64<LPC>(sd.t4);
+    // this lane's outputs: j0 .. j0+SPL-1 of the candidate's 8 (profile 0-3, DM 4-7)
+    const int j0 = sub * SPL;
+    const bool is_dm = j0 >= 4;
+    const RowSums& s = is_dm ? sd : sp;
+    const Moments m = moments_i64(L, s.t1, s.t2, s.t3, s.t4);
+    if (valid) {
+      double* o = out + c * 8 + j0;
+      if constexpr (SPL == 4) {
+        f64x2 a = {stat_k(m, 0), stat_k(m, 1)};
+        f64x2 b = {stat_k(m, 2), stat_k(m, 3)};
+        __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(o));
+        __builtin_nontemporal_store(b, reinterpret_cast<f64x2*>(o) + 1);
+      } else if constexpr (SPL == 2) {
+        const int k0 = j0 & 3;
+        f64x2 a = {stat_k(m, k0), stat_k(m, k0 + 1)};
+        __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(o));
+      } else {
+        __builtin_nontemporal_store(stat_k(m, j0 & 3), o);
+      }
+    }
+  }
+}
+
+// ---- generic path ----------------------------------------------------------------------
+// One wave per (candidate,row).  Rows of any length/alignment.
+__global__ __launch_bounds__(256) void lyon8_u8_generic(const uint8_t* __restrict__ prof,
+                                                        int64_t ps, int lp,
+                                                        const uint8_t* __restrict__ dm,
+                                                        int64_t ds, int ld, int64_t n,
+                                                        double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < 2 * n; w += nwaves) {
+    const int64_t c = w >> 1;
+    const int row = (int)(w & 1);
+    const uint8_t* p = row ? dm + c * ds : prof + c * ps;
+    const int len = row ? ld : lp;
+    long long t1 = 0, t2 = 0, t3 = 0;
+    unsigned long long t4 = 0;
+    for (int i = lane; i < len; i += 64) {
+      const int y = (int)p[i] - 128;
+      const int y2 = y * y;
+      t1 += y;
+      t2 += y2;
+      t3 += (long long)(y2 * y);
+      t4 += (unsigned long long)((uint32_t)y2 * (uint32_t)y2);
+    }
+    t1 = wave_sum_i64(t1);
+    t2 = wave_sum_i64(t2);
+    t3 = wave_sum_i64(t3);
+    t4 = (unsigned long long)wave_sum_i64((long long)t4);
+    if (lane < 4) {
+      const Moments m = len <= 430 ? moments_i64(len, t1, t2, t3, t4)
+                                   : moments_i128(len, t1, t2, t3, t4);
+      out[c * 8 + row * 4 + lane] = stat_k(m, lane);
+    }
+  }
+}
+
+// ---- fp64 rows (PFD) -------------------------------------------------------------------
+// Two-pass fp64, as numpy/scipy: mean = sum/n; m_k = mean((x-mean)^k) with d^3 = d^2*d and
+// d^4 = (d^2)^2 (scipy.stats._moment exponentiation by squares).  One wave per row.
+__global__ __launch_bounds__(256) void lyon8_f64_generic(const double* __restrict__ prof,
+                                                         int64_t ps, int lp,
+                                                         const double* __restrict__ dm,
+                                                         int64_t ds, int ld, int64_t n,
+                                                         double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < 2 * n; w += nwaves) {
+    const int64_t c = w >> 1;
+    const int row = (int)(w & 1);
+    const double* p = row ? dm + c * ds : prof + c * ps;
+    const int len = row ? ld : lp;
+    double s = 0.0;
+    for (int i = lane; i < len; i += 64) s += p[i];
+    s = wave_sum_f64(s);
+    const double mean = s / (double)len;
+    double a2 = 0.0, a3 = 0.0, a4 = 0.0;
+    for (int i = lane; i < len; i += 64) {
+      const double d = p[i] - mean;
+      const double d2 = d * d;
+      a2 += d2;
+      a3 += d2 * d;
+      a4 += d2 * d2;
+    }
+    a2 = wave_sum_f64(a2);
+    a3 = wave_sum_f64(a3);
+    a4 = wave_sum_f64(a4);
+    if (lane < 4) {
+      Moments m;
+      m.mean = mean;
+      m.m2 = a2 / (double)len;
+      m.m3 = a3 / (double)len;
+      m.m4 = a4 / (double)len;
+      out[c * 8 + row * 4 + lane] = stat_k(m, lane);
+    }
+  }
+}
+
+}  // namespace pfe
+
+// ---- launchers (called from capi.cpp) ---------------------------------------------------
+namespace pfe {
+
+static inline int grid_for(int64_t work_waves) {
+  // 4 waves per block; cap at 256 CUs x 8 blocks and grid-stride the rest.
+  int64_t blocks = (work_waves + 3) / 4;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  return (int)blocks;
+}
+
+hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
+                           int64_t ds, int ld, int64_t n, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const bool aligned = ((uintptr_t)prof % 16 == 0) && ((uintptr_t)dm % 16 == 0) &&
+                       (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
+    const int cpw = 64 / (lp / 32);
+    const int grid = grid_for((n + cpw - 1) / cpw);
+    if (lp == 64)
+      hipLaunchKernelGGL(lyon8_u8_fast<64>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+    else if (lp == 128)
+      hipLaunchKernelGGL(lyon8_u8_fast<128>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+    else
+      hipLaunchKernelGGL(lyon8_u8_fast<256>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+  } else {
+    const int grid = grid_for(2 * n);
+    hipLaunchKernelGGL(lyon8_u8_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_lyon8_f64(const double* prof, int64_t ps, int lp, const double* dm,
+                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int grid = grid_for(2 * n);
+  hipLaunchKernelGGL(lyon8_f64_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace pfe

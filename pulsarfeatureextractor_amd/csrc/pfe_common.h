@@ -1,0 +1,79 @@
+// pfe_common.h — shared device helpers for the gfx950 kernels of libpfe.so.
+//
+// Wave-level (64-lane) reductions are written with DPP row operations
+// (__builtin_amdgcn_update_dpp) for the in-row steps and ds_swizzle/readlane-free
+// cross-row steps, so no LDS round trip is needed.  Everything here assumes wave64.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PFE_WAVE 64
+
+namespace pfe {
+
+// ---- DPP controls (gfx9 encoding) ----------------------------------------------------
+// quad_perm selectors: ctrl = p0 | p1<<2 | p2<<4 | p3<<6
+constexpr int DPP_QUAD_XOR1 = 0xB1;  // [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;  // [2,3,0,1]
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;  // lane i <-> 7-i within each 8-lane half-row
+constexpr int DPP_ROW_MIRROR = 0x140;       // lane i <-> 15-i within each 16-lane row
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const int lo = dpp_i32<CTRL>((int)(uint32_t)v);
+  const int hi = dpp_i32<CTRL>((int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  return __longlong_as_double((long long)dpp_u64<CTRL>((uint64_t)__double_as_longlong(v)));
+}
+
+// Butterfly all-reduce (sum) over aligned groups of G lanes, G in {1,2,4,8,16}.
+// After the call every lane of the group holds the group total.
+template <int G>
+__device__ __forceinline__ int group_sum_i32(int v) {
+  if constexpr (G >= 2) v += dpp_i32<DPP_QUAD_XOR1>(v);
+  if constexpr (G >= 4) v += dpp_i32<DPP_QUAD_XOR2>(v);
+  if constexpr (G >= 8) v += dpp_i32<DPP_ROW_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v += dpp_i32<DPP_ROW_MIRROR>(v);
+  return v;
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t group_sum_u64(uint64_t v) {
+  if constexpr (G >= 2) v += dpp_u64<DPP_QUAD_XOR1>(v);
+  if constexpr (G >= 4) v += dpp_u64<DPP_QUAD_XOR2>(v);
+  if constexpr (G >= 8) v += dpp_u64<DPP_ROW_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v += dpp_u64<DPP_ROW_MIRROR>(v);
+  return v;
+}
+
+// Full-wave sums (64 lanes).  The in-row part uses DPP; the two cross-row steps use
+// __shfl_xor (ds_bpermute), which is exact for integers and fixed-order for doubles, so
+// the result is identical in every lane and deterministic run to run.
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+  uint64_t u = group_sum_u64<16>((uint64_t)v);
+  u += (uint64_t)__shfl_xor((long long)u, 16);
+  u += (uint64_t)__shfl_xor((long long)u, 32);
+  return (long long)u;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dpp_f64<DPP_QUAD_XOR1>(v);
+  v += dpp_f64<DPP_QUAD_XOR2>(v);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f64<DPP_ROW_MIRROR>(v);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+}  // namespace pfe
