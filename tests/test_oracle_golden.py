@@ -1,0 +1,53 @@
+"""Pin the oracle against the reference's own outputs (tests/golden, tools/make_golden.py).
+
+The reference has no tests or fixtures of its own, so these vectors -- the
+reference itself run on synthetic PHCX/SUPERB files -- are the pin.
+
+Bar:
+  * Lyon-8: bit-exact (same numpy/scipy calls on the same rows).
+  * Bates-22: same failing candidates; bit-exact on every score except s10/s11; s10/s11
+    within 1e-5 relative in >= 70% of rows.  The reference is not bit-reproducible against
+    ITSELF on s10/s11: the same candidate scored twice in one process (different heap state)
+    moves s10/s11 in 4-18% of rows (last-bit differences inside numpy/MINPACK that the
+    8-pass double-Gaussian peel amplifies; measured), so no golden vector can
+    pin those two scores more tightly.
+"""
+import numpy as np
+import pytest
+
+from golden_util import SELF_NOISY, bates_inputs, load
+from oracle.bates import bates22
+from oracle.lyon import lyon8
+
+
+@pytest.mark.parametrize("name", ["lyon8_superb64", "lyon8_phcx128", "lyon8_phcx128_dmplane"])
+def test_lyon8_oracle_bit_exact(name):
+    d = load(name)
+    assert d["ok"].all()
+    got = lyon8(d["prof"], d["block0"])
+    ref = d["out"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    m = ~np.isnan(ref)
+    assert np.array_equal(got[m], ref[m])
+
+
+@pytest.mark.parametrize("name,rows", [("bates22_phcx128", 90), ("bates22_superb64", 45)])
+def test_bates22_oracle_vs_reference(name, rows):
+    d = load(name)
+    prof, sub, curve, scal = bates_inputs(d)
+    ok = d["ok"]
+    # every failing row plus a prefix of the set
+    sel = np.unique(np.concatenate([np.arange(rows), np.where(~ok)[0]]))
+    out, st = bates22(prof[sel], sub[sel], curve[sel], scal[sel])
+    assert np.array_equal((st & 0xFF) == 0, ok[sel]), "failure pattern differs"
+    m = ok[sel]
+    ref = d["out"][sel][m]
+    got = out[m]
+    same = (got == ref) | (np.isnan(got) & np.isnan(ref))
+    with np.errstate(all="ignore"):
+        close = same | (np.abs(got - ref) <= 1e-5 * np.abs(ref))
+    for j in range(22):
+        if j in SELF_NOISY:
+            assert close[:, j].mean() >= 0.70, f"s{j + 1}: {close[:, j].mean():.3f}"
+        else:
+            assert same[:, j].all(), f"s{j + 1} not bit-exact in {(~same[:, j]).sum()} rows"

@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Golden vectors from the REAL reference (run only in the build container).
+
+What it does:
+  1. copies PulsarFeatureExtractor/src/*.py from /root/reference into a temporary directory
+     (never into this repository), converts it with lib2to3 (fixers print, except, has_key,
+     long, numliterals) and applies the minimal compatibility patches below, which restore
+     the Python-2.7 semantics the reference was written for (.pydevproject:6);
+  2. writes synthetic PHCX (gzip, 128-bin, section 1) and SUPERB PHCX (plain, 64-bin,
+     section 0) candidate files with pulsarfeatureextractor_amd.phcx.write;
+  3. runs, in a child process inside that temporary directory,
+        Candidate(f, f).calculateProfileStatScores(False) + calculateDMCurveStatScores(False)
+        (the dmprof path, DataProcessor.py:882-886)  and
+        Candidate(f, f).calculateScores(False)       (the 22-score path, :505-510);
+  4. stores inputs (as arrays) and outputs under tests/golden/*.npz plus a JSON manifest
+     with numpy/scipy versions, seeds and the patch list.
+
+Compatibility patches (each restores Py2 behaviour, none changes the algorithm):
+  ProfileOperationsInterface.py  Py2 '/' on integers is floor division: nbins and scale()
+                                  use _py2div (scale() therefore returns 0 for every index,
+                                  so fitGaussianT1/fitDoubleGaussianT2 always rotate)
+  ProfileOperations.py           'from scipy import std' -> numpy.std (removed from scipy);
+                                  'xData == []' on an ndarray was False in 2014 numpy
+                                  (raises on numpy 2) -> _py2_eq_empty; ceil(L/2) -> L//2;
+                                  width_bins/2 -> width_bins//2 (Py2 int division)
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+REF_SRC = "/root/reference/PulsarFeatureExtractor/src"
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+HELPERS = '''
+import numpy as _np
+def _py2div(a, b):
+    """Python-2 '/' : floor division when both operands are integers."""
+    if isinstance(a, (int, _np.integer)) and isinstance(b, (int, _np.integer)) \\
+            and not isinstance(a, bool) and not isinstance(b, bool):
+        return a // b
+    return a / b
+def _py2_eq_empty(x):
+    """Python-2 era 'x == []': True only for an empty list."""
+    return isinstance(x, list) and len(x) == 0
+'''
+
+PATCHES = {
+    "ProfileOperationsInterface.py": [
+        ("from Utilities import Utilities", "from Utilities import Utilities\n" + HELPERS),
+        ("nbins = ceil( rnge / binwidth )", "nbins = ceil( _py2div(rnge, binwidth) )"),
+        ("x = (newMin * (1-( (x-min_) /( max_-min_ )))) + (newMax * ( (x-min_) /( max_-min_ ) ))",
+         "x = (newMin * (1-( _py2div((x-min_), ( max_-min_ ))))) + "
+         "(newMax * ( _py2div((x-min_), ( max_-min_ )) ))"),
+    ],
+    "ProfileOperations.py": [
+        ("from scipy import std", "from numpy import std"),
+        ("from ProfileOperationsInterface import ProfileOperationsInterface",
+         "from ProfileOperationsInterface import ProfileOperationsInterface, _py2div, _py2_eq_empty"),
+        ("if xData == []:", "if _py2_eq_empty(xData):"),
+        ("int(ceil(yDataLength/2))", "int(ceil(yDataLength//2))"),
+        ("max_bin = j+width_bins/2", "max_bin = j+width_bins//2"),
+    ],
+}
+
+RUNNER = r'''
+import json, sys, traceback, warnings
+warnings.simplefilter("ignore")
+import numpy as np
+import Candidate
+files = json.load(open(sys.argv[1]))
+mode = sys.argv[2]
+res = []
+for f in files:
+    try:
+        c = Candidate.Candidate(f, f)
+        if mode == "lyon8":
+            a = list(c.calculateProfileStatScores(False))
+            b = list(c.calculateDMCurveStatScores(False))
+            v = [float(x) for x in a + b]
+        else:
+            v = [float(x) for x in c.calculateScores(False)]
+        res.append({"ok": True, "v": v})
+    except Exception as e:
+        res.append({"ok": False, "err": "".join(traceback.format_exception_only(type(e), e)).strip()})
+json.dump(res, open(sys.argv[3], "w"))
+'''
+
+
+def build_reference(tmp: str) -> str:
+    dst = os.path.join(tmp, "ref")
+    os.makedirs(dst)
+    for fn in os.listdir(REF_SRC):
+        if fn.endswith(".py"):
+            shutil.copy(os.path.join(REF_SRC, fn), dst)
+    subprocess.run([sys.executable, "-m", "lib2to3", "-f", "print", "-f", "except", "-f",
+                    "has_key", "-f", "long", "-f", "numliterals", "-w", "-n", "."],
+                   cwd=dst, check=True, capture_output=True)
+    for fn, subs in PATCHES.items():
+        p = os.path.join(dst, fn)
+        s = open(p).read()
+        for a, b in subs:
+            if a not in s:
+                raise RuntimeError(f"patch anchor not found in {fn}: {a!r}")
+            s = s.replace(a, b)
+        open(p, "w").write(s)
+    with open(os.path.join(dst, "_runner.py"), "w") as f:
+        f.write(RUNNER)
+    return dst
+
+
+def run_reference(refdir: str, files: list[str], mode: str, tmp: str):
+    fl = os.path.join(tmp, f"files_{mode}.json")
+    out = os.path.join(tmp, f"out_{mode}.json")
+    json.dump(files, open(fl, "w"))
+    env = dict(os.environ, MPLBACKEND="Agg", PYTHONHASHSEED="0")
+    subprocess.run([sys.executable, "_runner.py", fl, mode, out], cwd=refdir, check=True, env=env)
+    return json.load(open(out))
+
+
+# ------------------------------------------------------------------------------------------
+# synthetic candidate sets
+# ------------------------------------------------------------------------------------------
+def lyon_set(rng, n, lp, l0, superb):
+    from pulsarfeatureextractor_amd.synth import _rows_numpy
+
+    prof = _rows_numpy(rng, n, lp, 150.0, 150.0)
+    dm0 = _rows_numpy(rng, n, l0, 150.0, 150.0)
+    # adversarial rows
+    prof[0] = 0
+    dm0[0] = 255
+    prof[1] = 77
+    prof[2] = 0
+    prof[2, 5] = 255
+    dm0[3] = 255
+    dm0[3, ::2] = 0
+    prof[4] = np.arange(lp) % 256
+    return prof, dm0
+
+
+def bates_set(rng, n, lp, nsub, lsb, ndm, superb):
+    from pulsarfeatureextractor_amd.phcx import make_datablock
+    from pulsarfeatureextractor_amd.synth import _rows_numpy
+
+    prof = _rows_numpy(rng, n, lp, 150.0, 150.0)
+    sub = _rows_numpy(rng, n * nsub, lsb, 20.0, 150.0).reshape(n, nsub, lsb)
+    curve = _rows_numpy(rng, n, ndm, 150.0, 150.0, pulsar_frac=1.0, centred=True)
+    period = rng.uniform(0.05, 1.0, size=n)
+    dmv = rng.uniform(10.0, 150.0, size=n)
+    snr = rng.uniform(8.0, 30.0, size=n)
+    width = rng.uniform(0.02, 0.1, size=n)
+    # adversarial rows
+    prof[0] = 50                 # constant profile: maxima=0 -> s1,s2 inf; histogram fallback
+    prof[1] = 0
+    prof[1, ::3] = 200           # comb: many peaks
+    prof[2] = 0
+    prof[2, lp // 2] = 255       # single spike
+    sub[3] = 0                   # all-zero sub-bands: corrcoef NaN everywhere -> m=0 -> fail
+    width[4] = 0.0               # width*Lsb = 0 -> boxcar width 0
+    width[5] = 1.0 / lsb * 3.0   # odd boxcar width 3
+    prof[6] = np.roll(prof[6], -int(np.argmax(prof[6])))  # peak at bin 0
+    prof[7] = np.roll(prof[7], lp - 1 - int(np.argmax(prof[7])))  # peak at the last bin
+    blocks = np.stack([make_datablock(curve[i], rng) for i in range(n)])
+    return prof, sub, curve, blocks, period, dmv, snr, width
+
+
+def write_files(d, kind, arrays, superb):
+    from pulsarfeatureextractor_amd import phcx
+
+    os.makedirs(d, exist_ok=True)
+    files = []
+    ext = ".phcx" if superb else ".phcx.gz"
+    for i in range(arrays["n"]):
+        p = os.path.join(d, f"{kind}_{i:05d}{ext}")
+        phcx.write(p, profile=arrays["prof"][i], subbands=arrays["sub"][i],
+                   datablocks=(arrays["block0"][i], arrays["block1"][i]),
+                   dm_start=arrays["dm_start"], dm_end=arrays["dm_end"],
+                   n_dm_index=arrays["n_dm_index"], period_s=float(arrays["period"][i]),
+                   snr=float(arrays["snr"][i]), dm=float(arrays["dm"][i]),
+                   width=float(arrays["width"][i]), superb=superb)
+        files.append(p)
+    return files
+
+
+def collect(res, nout):
+    n = len(res)
+    out = np.full((n, nout), np.nan)
+    ok = np.zeros(n, dtype=bool)
+    errs = []
+    for i, r in enumerate(res):
+        ok[i] = r["ok"]
+        if r["ok"]:
+            out[i] = r["v"]
+            errs.append("")
+        else:
+            errs.append(r["err"])
+    return out, ok, np.array(errs)
+
+
+def main():
+    import scipy
+
+    os.makedirs(GOLDEN, exist_ok=True)
+    manifest = {"numpy": np.__version__, "scipy": scipy.__version__,
+                "python": sys.version.split()[0], "reference": REF_SRC,
+                "patches": {k: [a for a, _ in v] for k, v in PATCHES.items()},
+                "lib2to3_fixers": ["print", "except", "has_key", "long", "numliterals"],
+                "sets": {}}
+    with tempfile.TemporaryDirectory(prefix="pfe_golden_") as tmp:
+        refdir = build_reference(tmp)
+        specs = [
+            # name, mode, superb, n, lp, l0 (Lyon DM length), nsub, lsb, ndm, seed
+            ("lyon8_superb64", "lyon8", True, 400, 64, 64, 16, 64, 2, 1),
+            ("lyon8_phcx128", "lyon8", False, 400, 128, 128, 16, 128, 2, 2),
+            ("lyon8_phcx128_dmplane", "lyon8", False, 60, 128, 120 * 128, 16, 128, 2, 3),
+            ("bates22_phcx128", "bates22", False, 300, 128, 128, 16, 128, 128, 4),
+            ("bates22_superb64", "bates22", True, 150, 64, 64, 16, 64, 120, 5),
+        ]
+        for name, mode, superb, n, lp, l0, nsub, lsb, ndm, seed in specs:
+            rng = np.random.default_rng(20261015 + 100 * seed)
+            if mode == "lyon8":
+                prof, dm0 = lyon_set(rng, n, lp, l0, superb)
+                from pulsarfeatureextractor_amd.phcx import make_datablock
+                from pulsarfeatureextractor_amd.synth import _rows_numpy
+                sub = _rows_numpy(rng, n * nsub, lsb, 20.0, 150.0).reshape(n, nsub, lsb)
+                curve = _rows_numpy(rng, n, ndm, 150.0, 150.0, pulsar_frac=1.0, centred=True)
+                block1 = np.stack([make_datablock(curve[i], rng) for i in range(n)])
+                arrays = dict(n=n, prof=prof, sub=sub, block0=dm0,
+                              block1=dm0 if superb else block1,
+                              period=rng.uniform(0.05, 1.0, n), dm=rng.uniform(10, 150, n),
+                              snr=rng.uniform(8, 30, n), width=rng.uniform(0.02, 0.1, n),
+                              dm_start=0.0, dm_end=200.0, n_dm_index=101)
+            else:
+                prof, sub, curve, blocks, period, dmv, snr, width = bates_set(
+                    rng, n, lp, nsub, lsb, ndm, superb)
+                b0 = blocks if superb else _rows_lyon(rng, n, 128)
+                arrays = dict(n=n, prof=prof, sub=sub, block0=b0, block1=blocks,
+                              period=period, dm=dmv, snr=snr, width=width,
+                              dm_start=0.0, dm_end=200.0, n_dm_index=101)
+            files = write_files(os.path.join(tmp, name), name, arrays, superb)
+            res = run_reference(refdir, files, mode, tmp)
+            nout = 8 if mode == "lyon8" else 22
+            out, ok, errs = collect(res, nout)
+            np.savez_compressed(
+                os.path.join(GOLDEN, name + ".npz"),
+                prof=arrays["prof"].astype(np.uint8), sub=arrays["sub"].astype(np.uint8),
+                block0=np.asarray(arrays["block0"]).astype(np.uint8),
+                block1=np.asarray(arrays["block1"]).astype(np.uint8),
+                period=arrays["period"], dm=arrays["dm"], snr=arrays["snr"],
+                width=arrays["width"], dm_start=arrays["dm_start"], dm_end=arrays["dm_end"],
+                n_dm_index=arrays["n_dm_index"], superb=superb, out=out, ok=ok, err=errs)
+            manifest["sets"][name] = {"mode": mode, "superb": superb, "n": n, "lp": lp,
+                                      "lyon_dm_len": l0, "nsub": nsub, "lsb": lsb, "ndm": ndm,
+                                      "seed": 20261015 + 100 * seed,
+                                      "failures": int((~ok).sum())}
+            print(f"{name}: {n} candidates, {int((~ok).sum())} reference failures", flush=True)
+    with open(os.path.join(GOLDEN, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+def _rows_lyon(rng, n, L):
+    from pulsarfeatureextractor_amd.synth import _rows_numpy
+
+    return _rows_numpy(rng, n, L, 150.0, 150.0)
+
+
+if __name__ == "__main__":
+    main()
