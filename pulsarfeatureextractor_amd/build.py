@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 BUILDDIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIBDIR, "libpfe.so")
-SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip"]
+SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip"]
 ARCH = os.environ.get("PFE_OFFLOAD_ARCH", "gfx950")
 
 

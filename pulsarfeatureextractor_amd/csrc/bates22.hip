@@ -1,9 +1,59 @@
-// bates22.hip — placeholder launcher (filled in by the Bates-score kernels).
-#include <hip/hip_runtime.h>
-#include "../../include/pfe.h"
+// bates22.hip — host launcher of the 22-score pipeline (PHCXFile.compute, PHCXFile.py:383-409).
+//
+// Score groups run as separate kernels on the caller's stream, in the reference's group
+// order; each writes its own output columns and ORs its failure bit into status[c]:
+//   k_sine (s1-s4) -> k_ghist (+ k_ghist<BIG> for wide histograms) -> k_gt1 (s8,s9)
+//   -> k_gdg (s10,s11) -> k_dmfit (s12-s19) -> k_subband (s20-s22)
+#include <cmath>
+
+#include "bates_common.h"
+
 namespace pfe {
-size_t bates22_workspace_bytes(const pfe_bates_in*) { return 0; }
-hipError_t launch_bates22(const pfe_bates_in*, double*, uint32_t*, void*, size_t, hipStream_t) {
-  return hipErrorNotSupported;
+
+hipError_t launch_sine(const BatesArgs& a, hipStream_t st);
+hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
+hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st);
+hipError_t launch_subband(const BatesArgs& a, hipStream_t st);
+
+size_t bates22_workspace_bytes(const pfe_bates_in* in) {
+  return (size_t)in->n * sizeof(GaussWS) + 256;
 }
+
+__global__ void k_clear_internal(uint32_t* status, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) status[i] &= 0xFFFFu;
+}
+
+hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                          size_t work_bytes, hipStream_t st) {
+  if (work_bytes < bates22_workspace_bytes(in)) return hipErrorInvalidValue;
+  BatesArgs a;
+  a.prof = in->prof;
+  a.lp = in->lp;
+  a.sub = in->sub;
+  a.nsub = in->nsub;
+  a.lsb = in->lsb;
+  a.dmcurve = in->dmcurve;
+  a.ndm = in->ndm;
+  a.scal = in->scal;
+  a.n = in->n;
+  a.out = out;
+  a.status = status;
+  a.ws = (GaussWS*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
+  // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code
+  a.c_lp = std::pow((double)in->lp, -0.3333333);
+  a.c_lp1 = std::pow((double)(in->lp - 1), -0.3333333);
+  hipError_t e = hipMemsetAsync(status, 0, (size_t)in->n * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(out, 0, (size_t)in->n * 22 * sizeof(double), st);
+  if (e != hipSuccess) return e;
+  if ((e = launch_sine(a, st)) != hipSuccess) return e;
+  if ((e = launch_gauss(a, st)) != hipSuccess) return e;
+  if ((e = launch_dmfit(a, st)) != hipSuccess) return e;
+  if ((e = launch_subband(a, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_clear_internal, dim3((unsigned)((in->n + 255) / 256)), dim3(256), 0, st,
+                     status, in->n);
+  return hipGetLastError();
+}
+
 }  // namespace pfe

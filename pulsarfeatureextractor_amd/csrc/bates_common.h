@@ -1,0 +1,103 @@
+// bates_common.h — shared pieces of the 22-score kernels (one wavefront per candidate).
+#pragma once
+
+#include "../../include/pfe.h"
+#include "lm_wave.h"
+
+namespace pfe {
+
+#pragma clang fp contract(off)
+
+constexpr double TWO_PI = 6.283185307179586;          // Python's 2*pi (numpy.pi * 2)
+constexpr double FWHM_C = 2.3548200450309493;         // 2*sqrt(2*log(2)) as numpy computes it
+constexpr int BLOCK = 256;                            // 4 waves = 4 candidates per block
+
+// internal status bits (not exported)
+constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
+constexpr uint32_t PFE_ST_UNSUPPORTED = 0x010u;
+
+// per-candidate workspace passed between the Gaussian-group kernels
+struct GaussWS {
+  double p_mu;      // mu of the Gaussian fit to the profile histogram   (:681-682)
+  double minbg;     // min(p_mu, mean(profile))                          (:724)
+  double pstd;      // profile.std()
+  double t1[4];     // fitGaussianT1 parameters (sigma, mu, A, bg)       (:739, :1246)
+  double pad;
+};
+
+struct BatesArgs {
+  const uint8_t* prof;
+  int lp;
+  const uint8_t* sub;
+  int nsub, lsb;
+  const double* dmcurve;
+  int ndm;
+  const double* scal;
+  int64_t n;
+  double* out;       // n x 22
+  uint32_t* status;  // n
+  GaussWS* ws;       // n
+  double c_lp;       // pow(lp, -0.3333333)     (ProfileOperationsInterface.py:151)
+  double c_lp1;      // pow(lp-1, -0.3333333)
+};
+
+__device__ __forceinline__ int64_t wave_candidate() {
+  return ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+}
+
+// Profile row of candidate c into MPL slots (rows beyond lp read 0).
+template <int MPL>
+__device__ __forceinline__ void load_row_u8(const uint8_t* row, int len, int lane, int (&v)[MPL]) {
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    v[k] = (i < len) ? (int)row[i] : 0;
+  }
+}
+
+// numpy mean / std (ddof=0) of an integer row from exact integer sums.
+struct MeanStd {
+  double mean, std;
+};
+template <int MPL>
+__device__ __forceinline__ MeanStd int_mean_std(const int (&v)[MPL], int len, int lane) {
+  long long s1 = 0, s2 = 0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (lane + 64 * k < len) {
+      s1 += v[k];
+      s2 += (long long)v[k] * v[k];
+    }
+  s1 = wsum_ll(s1);
+  s2 = wsum_ll(s2);
+  const double n = (double)len;
+  const double mean = (double)s1 / n;
+  const long long N2 = (long long)len * s2 - s1 * s1;  // exact for len*255^2*len < 2^63
+  return {mean, sqrt((double)N2 / (n * n))};
+}
+
+// numpy mean / std of a distributed float vector (two-pass, tree sums)
+struct FMeanStd {
+  double mean, std;
+};
+template <int MPL>
+__device__ __forceinline__ FMeanStd f_mean_std(const double (&v)[MPL], const bool (&ok)[MPL], int len) {
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (ok[k]) s += v[k];
+  const double mean = wsum(s) / (double)len;
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (ok[k]) {
+      const double d = v[k] - mean;
+      q += d * d;
+    }
+  return {mean, sqrt(wsum(q) / (double)len)};
+}
+
+// Python's builtin min(a, b): returns a unless b < a
+__device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
+
+}  // namespace pfe

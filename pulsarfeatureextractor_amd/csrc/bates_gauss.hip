@@ -1,0 +1,786 @@
+// bates_gauss.hip — scores 5-11 (Gaussian fits) on gfx950, one wavefront per candidate.
+//
+// Reference: ProfileOperations.getGaussianFittings (PulsarFeatureExtractor/src/
+// ProfileOperations.py:595-770) with freedmanDiaconisRule / getDerivative
+// (ProfileOperationsInterface.py:138-186), numpy.histogram, fitGaussian :774-983,
+// fitGaussianFixedWidthBins :988-1057, fitGaussianT1 :1061-1132 ->
+// fitGaussianWithBackground :1194-1264, fitDoubleGaussianT2 :1136-1190 ->
+// fitDoubleGaussian :1268-1428 -> fitDoubleGaussianWithBackground :1432-1483.
+//
+// Three kernels (launched in this order on one stream):
+//   k_ghist  : Freedman-Diaconis bin counts, the two histograms and their Gaussian fits
+//              -> s5, s6, s7 and mu of the profile-histogram fit (workspace)
+//   k_gt1    : background-subtracted, half-rotated profile, 4-parameter fit -> s8, s9
+//   k_gdg    : peak peeling, 8 single-Gaussian passes with subtraction, the 8-parameter
+//              fit and the combination rule -> s10, s11
+#include "bates_common.h"
+
+namespace pfe {
+
+#pragma clang fp contract(off)
+
+// ---------------------------------------------------------------------------------------
+// order statistics of small integer data by bisection over the value range (ballots)
+// ---------------------------------------------------------------------------------------
+template <int MPL>
+__device__ int kth_smallest(const int (&v)[MPL], const bool (&ok)[MPL], int k, int lo, int hi) {
+  // smallest x in [lo, hi] with #(v <= x) >= k+1
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;  // floor (arithmetic shift)
+    int cnt = 0;
+#pragma unroll
+    for (int s = 0; s < MPL; ++s) cnt += __popcll(__ballot(ok[s] && v[s] <= mid));
+    if (cnt >= k + 1)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
+
+// scipy.stats.scoreatpercentile(data, per), interpolation 'fraction'
+template <int MPL>
+__device__ double score_at_percentile(const int (&v)[MPL], const bool (&ok)[MPL], int n, double per,
+                                      int lo, int hi) {
+  const double idx = per / 100.0 * (double)(n - 1);
+  const int i = (int)idx;
+  if ((double)i == idx) return (double)kth_smallest<MPL>(v, ok, i, lo, hi);
+  const double w0 = (double)(i + 1) - idx, w1 = idx - (double)i;
+  const double si = (double)kth_smallest<MPL>(v, ok, i, lo, hi);
+  const double sj = (double)kth_smallest<MPL>(v, ok, i + 1, lo, hi);
+  return (si * w0 + sj * w1) / (w0 + w1);
+}
+
+// freedmanDiaconisRule (ProfileOperationsInterface.py:138-166).  c = pow(n, -0.3333333)
+// computed on the host with the C library pow, as Python does.
+template <int MPL>
+__device__ int fd_bins(const int (&v)[MPL], const bool (&ok)[MPL], int n, double c, int vmin, int vmax) {
+  const double iqr = score_at_percentile<MPL>(v, ok, n, 75.0, vmin, vmax) -
+                     score_at_percentile<MPL>(v, ok, n, 25.0, vmin, vmax);
+  const double bw = 2.0 * iqr * c;
+  const int rng = vmax - vmin;
+  if (bw <= 0.0) return rng / 60;  // binwidth = 60 (int); Py2 int '/' floors
+  const double q = ceil((double)rng / bw);
+  return q > 1e9 ? 1000000000 : (int)q;
+}
+
+// numpy.histogram(data, nbins) of integers into per-wave LDS counters
+struct HistSpec {
+  double first, last, step;
+  int nb;
+  __device__ double edge(int i) const { return i >= nb ? last : (double)i * step + first; }
+};
+
+__device__ __forceinline__ HistSpec hist_spec(int vmin, int vmax, int nb) {
+  HistSpec h;
+  h.first = (double)vmin;
+  h.last = (double)vmax;
+  if (vmin == vmax) {
+    h.first -= 0.5;
+    h.last += 0.5;
+  }
+  h.nb = nb;
+  h.step = (h.last - h.first) / (double)nb;  // numpy.linspace: delta/div, then i*step + start
+  return h;
+}
+
+__device__ __forceinline__ int hist_bin(const HistSpec& h, int iv) {
+  const double v = (double)iv;
+  const double denom = (double)(h.last - h.first);
+  int idx = (int)(((v - h.first) / denom) * (double)h.nb);
+  if (idx == h.nb) idx -= 1;
+  if (v < h.edge(idx)) idx -= 1;
+  if (v >= h.edge(idx + 1) && idx != h.nb - 1) idx += 1;
+  return idx;
+}
+
+// ---------------------------------------------------------------------------------------
+// Gaussian fit to a histogram (fitGaussian :774-983)
+// ---------------------------------------------------------------------------------------
+template <int MPL>
+struct GaussFn {  // y - |A| exp(-((x-mu)/sigma)^2 / 2)
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  __device__ double model(const double (&p)[3], int k) const {
+    const double t = (x[k] - p[1]) / p[0];
+    return fabs(p[2]) * exp(-(t * t) / 2.0);
+  }
+  __device__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+};
+
+template <int MPL>
+struct GaussFixedFn {  // mu fixed at xmax; parameters (sigma, A)
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  double xmax;
+  __device__ double model(const double (&p)[2], int k) const {
+    const double t = (x[k] - xmax) / p[0];
+    return fabs(p[1]) * exp(-(t * t) / 2.0);
+  }
+  __device__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+};
+
+struct HistFit {
+  double sigma, mu, amp;
+  bool fail;  // IndexError / ValueError / TypeError in the reference
+};
+
+// counts in y (nb bins, left edges in x); returns the final parameters
+template <int MPL>
+__device__ HistFit fit_gaussian_hist(GaussFn<MPL>& fn, int nb, int lane) {
+  HistFit r{0, 0, 0, false};
+  // statistics of the (unpadded) counts
+  double cmax = -1.0;
+  int imax = 1 << 30;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (lane + 64 * k < nb) {
+      s += fn.y[k];
+      if (fn.y[k] > cmax) {
+        cmax = fn.y[k];
+        imax = lane + 64 * k;
+      }
+    }
+  const ArgMax am = wargmax(cmax, imax);
+  const int idx = am.i;
+  const double a0 = am.v;
+  const double mean = wsum(s) / (double)nb;
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (lane + 64 * k < nb) {
+      const double d = fn.y[k] - mean;
+      q += d * d;
+    }
+  const double s0 = sqrt(wsum(q) / (double)nb);
+  const double meansq = mean * mean;
+  const int nx = nb;
+  const int m = nb < 3 ? 3 : nb;  // zero-padded to the parameter count (:943-947)
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    fn.ok[k] = i < m;
+    if (i >= nb) {
+      fn.x[k] = 0.0;
+      fn.y[k] = 0.0;
+    }
+  }
+  // left edge of bin idx (x values live in lanes)
+  auto xat = [&](int i) -> double {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+      if (i >> 6 == k) v = bcast(fn.x[k], i & 63);
+    return v;
+  };
+  double mu0 = xat(idx);
+  int retry = 0;
+  double p[3];
+  for (;;) {
+    p[0] = s0;
+    p[1] = mu0;
+    p[2] = a0;
+    lmdif<3, MPL>(fn, p, 200 * 4);
+    double cs = 0.0;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+      if (lane + 64 * k < nx) {
+        const double d = fn.y[k] - fn.model(p, k);
+        cs += d * d;
+      }
+    const double chisq = wsum(cs) / (double)m;
+    if ((chisq > meansq * (double)nx) && (p[0] < 0.2 * (double)nx)) {
+      ++retry;
+      // temp = delete(temp, idx): after r deletions temp = counts[:idx] + counts[idx+r:]
+      if (idx + retry > nb) {  // numpy.delete index out of bounds
+        r.fail = true;
+        return r;
+      }
+      double bv = -1.0;
+      int bi = 1 << 30;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k) {
+        const int i = lane + 64 * k;
+        if (i < nb && (i < idx || i >= idx + retry) && fn.y[k] > bv) {
+          bv = fn.y[k];
+          bi = i;
+        }
+      }
+      const ArgMax t = wargmax(bv, bi);
+      if (t.i >= (1 << 30)) {  // argmax of an empty array
+        r.fail = true;
+        return r;
+      }
+      const int pos = t.i < idx ? t.i : t.i - retry;
+      if (pos + retry >= m) {  // xData[pos+counter] out of range
+        r.fail = true;
+        return r;
+      }
+      mu0 = xat(pos + retry);
+      if (retry > 5) break;
+    } else {
+      break;
+    }
+  }
+  r.sigma = p[0];
+  r.mu = p[1];
+  r.amp = p[2];
+  return r;
+}
+
+template <int MPL>
+__device__ void load_hist(GaussFn<MPL>& fn, const int* hist, const HistSpec& h, int lane) {
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    fn.ok[k] = i < h.nb;
+    fn.x[k] = i < h.nb ? h.edge(i) : 0.0;
+    fn.y[k] = i < h.nb ? (double)hist[i] : 0.0;
+  }
+}
+
+// P = slots of the profile (lp <= 64*P), H = histogram-bin slots (nb <= 64*H)
+template <int P, int H, bool BIG>
+__global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
+  __shared__ int hist_all[BLOCK / 64][64 * H];
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if constexpr (BIG) {
+    if (!(a.status[c] & ST_DEFER_HIST)) return;
+  }
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  int* hist = hist_all[wv];
+  const int lp = a.lp;
+  const uint8_t* row = a.prof + c * lp;
+  int v[P], d[P];
+  bool okv[P], okd[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    okv[k] = i < lp;
+    okd[k] = i < lp - 1;
+    v[k] = okv[k] ? (int)row[i] : 0;
+    d[k] = okd[k] ? (int)row[i] - (int)row[i + 1] : 0;  // getDerivative (:170-186)
+  }
+  int vmin = 1 << 30, vmax = -(1 << 30), dmin = 1 << 30, dmax = -(1 << 30);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    if (okv[k]) {
+      vmin = min(vmin, v[k]);
+      vmax = max(vmax, v[k]);
+    }
+    if (okd[k]) {
+      dmin = min(dmin, d[k]);
+      dmax = max(dmax, d[k]);
+    }
+  }
+  vmin = wmin_i(vmin);
+  vmax = wmax_i(vmax);
+  dmin = wmin_i(dmin);
+  dmax = wmax_i(dmax);
+  const int hb = fd_bins<P>(v, okv, lp, a.c_lp, vmin, vmax);        // :654
+  const int db = fd_bins<P>(d, okd, lp - 1, a.c_lp1, dmin, dmax);   // :656
+  uint32_t st = 0;
+  if (hb <= 0 || db <= 0) st = PFE_ST_GAUSS_FAIL;                  // histogram(bins=0) raises
+  if (!st && (hb > 64 * H || db > 64 * H)) st = BIG ? PFE_ST_UNSUPPORTED : ST_DEFER_HIST;
+  if (BIG && lane == 0) a.status[c] &= ~ST_DEFER_HIST;
+  if (st) {
+    if (lane == 0) a.status[c] |= st;
+    return;
+  }
+  // ---- derivative histogram and its fit (:657-661)
+  const HistSpec hd = hist_spec(dmin, dmax, db);
+  for (int i = lane; i < db; i += 64) hist[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (okd[k]) atomicAdd(&hist[hist_bin(hd, d[k])], 1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  GaussFn<H> fn;
+  load_hist<H>(fn, hist, hd, lane);
+  const HistFit fd = fit_gaussian_hist<H>(fn, db, lane);
+  // ---- profile histogram and its fits (:678-705)
+  __builtin_amdgcn_wave_barrier();
+  const HistSpec hp = hist_spec(vmin, vmax, hb);
+  for (int i = lane; i < hb; i += 64) hist[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (okv[k]) atomicAdd(&hist[hist_bin(hp, v[k])], 1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  load_hist<H>(fn, hist, hp, lane);
+  GaussFixedFn<H> fx;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    fx.x[k] = fn.x[k];
+    fx.y[k] = fn.y[k];
+    fx.ok[k] = fn.ok[k];
+  }
+  const HistFit fp = fit_gaussian_hist<H>(fn, hb, lane);
+  if (fd.fail || fp.fail || hb < 2) {  // hb < 2: leastsq(m=1 < n=2) raises TypeError
+    if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
+    return;
+  }
+  // fixed-mean fit (:1034-1045): xmax = xData[int(bins/2)-1] (index -1 = last bin)
+  int xi = hb / 2 - 1;
+  if (xi < 0) xi += hb;
+  fx.xmax = hp.edge(xi);
+  double cmax = -1.0, s = 0.0;
+#pragma unroll
+  for (int k = 0; k < H; ++k)
+    if (fx.ok[k]) {
+      cmax = fmax(cmax, fx.y[k]);
+      s += fx.y[k];
+    }
+  cmax = wmax(cmax);
+  const double mean = wsum(s) / (double)hb;
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < H; ++k)
+    if (fx.ok[k]) q += (fx.y[k] - mean) * (fx.y[k] - mean);
+  double pf[2] = {sqrt(wsum(q) / (double)hb), cmax};
+  lmdif<2, H>(fx, pf, 200 * 3);
+  const MeanStd ms = int_mean_std<P>(v, lp, lane);
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[4] = fabs(fx.xmax - fp.mu);          // s5 (:715)
+    o[5] = fabs(pf[1] / fp.amp);           // s6 (:716)
+    o[6] = fabs(fd.mu - fp.mu);            // s7 (:717)
+    GaussWS* w = a.ws + c;
+    w->p_mu = fp.mu;
+    w->minbg = py_min(fp.mu, ms.mean);     // :724
+    w->pstd = ms.std;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// s8, s9: fitGaussianT1 -> fitGaussianWithBackground
+// ---------------------------------------------------------------------------------------
+template <int MPL>
+struct GaussBgFn {  // y - (|A| exp(-((x-mu)/|sigma|)^2/2) + bg)      (:1226)
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  __device__ double model(const double (&p)[4], int k) const {
+    const double t = (x[k] - p[1]) / fabs(p[0]);
+    return fabs(p[2]) * exp(-(t * t) / 2.0) + p[3];
+  }
+  __device__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+};
+
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  const int lane = lane_id();
+  const int lp = a.lp;
+  const int cut = lp / 2;  // Py2: ceil(L/2) of an int division is L//2
+  const GaussWS w = a.ws[c];
+  GaussBgFn<P> fn;
+  bool ok[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    ok[k] = i < lp;
+    fn.ok[k] = ok[k];
+    fn.x[k] = (double)i;
+    double y = 0.0;
+    if (ok[k]) {
+      const int src = (i + cut) % lp;  // rotated: part2 + part1 (:1107-1109)
+      const double pv = (double)a.prof[c * lp + src];
+      if (w.minbg > 0.0) {
+        y = pv - w.minbg + w.pstd;      // :730
+        if (y < 0.0) y = 0.0;
+      } else {
+        y = pv;
+      }
+    }
+    fn.y[k] = y;
+  }
+  // initial parameters (:1239-1245)
+  double bv = -INFINITY;
+  int bi = 1 << 30;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k] && (bi == (1 << 30) || fn.y[k] > bv)) {
+      bv = fn.y[k];
+      bi = lane + 64 * k;
+    }
+  const ArgMax am = wargmax(bv, bi);
+  const FMeanStd fs = f_mean_std<P>(fn.y, ok, lp);
+  double p[4] = {fs.std, (double)am.i, am.v, 1.0};
+  lmdif<4, P>(fn, p, 200 * 5);
+  double cs = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k]) {
+      const double dd = fn.y[k] - fn.model(p, k);
+      cs += dd * dd;
+    }
+  const double chisq = wsum(cs) / (double)lp;
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[7] = fabs(FWHM_C * p[0]);  // s8 (:1247)
+    o[8] = chisq;                // s9
+    GaussWS* wp = a.ws + c;
+    wp->t1[0] = p[0];
+    wp->t1[1] = p[1];
+    wp->t1[2] = p[2];
+    wp->t1[3] = p[3];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// s10, s11: fitDoubleGaussianT2 -> fitDoubleGaussian -> fitDoubleGaussianWithBackground
+// ---------------------------------------------------------------------------------------
+template <int MPL>
+struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  __device__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      if (ok[k]) {
+        const double t = (x[k] - p[1]) / p[0];
+        f[k] = y[k] - (fabs(p[2]) * exp(-(t * t) / 2.0) + fabs(p[3]));
+      } else {
+        f[k] = 0.0;
+      }
+    }
+  }
+};
+__device__ __forceinline__ double g_absbg(double x, const double (&p)[4]) {
+  const double t = (x - p[1]) / p[0];
+  return fabs(p[2]) * exp(-(t * t) / 2.0) + fabs(p[3]);
+}
+
+template <int MPL>
+struct DoubleGaussFn {  // :1459-1460
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  __device__ double model(const double (&p)[8], int k) const {
+    const double t1 = (x[k] - p[1]) / fabs(p[0]);
+    const double t2 = (x[k] - p[5]) / fabs(p[4]);
+    return (fabs(p[2]) * exp(-(t1 * t1) / 2.0)) + (fabs(p[6]) * exp(-(t2 * t2) / 2.0)) +
+           (fabs(p[3]) + fabs(p[7])) / 2.0;
+  }
+  __device__ void operator()(const double (&p)[8], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+};
+
+// numpy.delete on the "kept" index list represented as a bit mask over original positions
+template <int P>
+struct KeptSet {
+  uint64_t w[P];
+  int len;
+  __device__ void init(int L) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int lo = 64 * j;
+      w[j] = (L >= lo + 64) ? ~0ull : (L > lo ? ((1ull << (L - lo)) - 1ull) : 0ull);
+    }
+    len = L;
+  }
+  // remove the element at (possibly negative) position pos of the compacted list;
+  // false = IndexError
+  __device__ bool del(int pos) {
+    if (pos < -len || pos >= len) return false;
+    if (pos < 0) pos += len;
+    int acc = 0;
+    bool done = false;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int cnt = __popcll(w[j]);
+      if (!done && pos < acc + cnt) {
+        uint64_t x = w[j];
+        for (int r = pos - acc; r > 0; --r) x &= x - 1;  // drop the r lowest set bits
+        w[j] &= ~(x & (~x + 1));                        // clear the next set bit
+        done = true;
+      }
+      acc += cnt;
+    }
+    --len;
+    return true;
+  }
+};
+
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
+  __shared__ int ys_all[BLOCK / 64][64 * P];
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  const int lane = lane_id();
+  const int L = a.lp;
+  const int cut = L / 2;
+  int* ys = ys_all[threadIdx.x >> 6];
+  // rotated integer profile (fitDoubleGaussianT2 :1162-1170)
+  int y[P];
+  bool ok[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    ok[k] = i < L;
+    y[k] = ok[k] ? (int)a.prof[c * L + (i + cut) % L] : -1;
+    if (ok[k]) ys[i] = y[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int bv = -1, bi = 1 << 30;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k] && y[k] > bv) {
+      bv = y[k];
+      bi = lane + 64 * k;
+    }
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const int ov = __shfl_xor(bv, s), oi = __shfl_xor(bi, s);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  const int pos = uni(bi);
+  // ---- neighbour peeling (:1305-1354), simulated on the kept-index mask
+  KeptSet<P> ks;
+  ks.init(L);
+  bool index_error = !ks.del(pos);
+  {
+    int tol = 0;
+    const int lim = 5;
+    int i = 1;
+    while (!index_error && i < L) {
+      if ((pos - i) > 0 && (pos + i) < L) {
+        const bool A = ys[pos - i] >= ys[pos - i + 1];
+        const bool B = ys[pos + i] >= ys[pos + i - 1];
+        if (!A && !B) {
+          index_error = !ks.del(pos - i) || !ks.del(pos - i);
+        } else if (A || (B && (tol < lim))) {
+          index_error = !ks.del(pos - i) || !ks.del(pos - i);
+          ++tol;
+        } else {
+          break;
+        }
+      } else if ((pos - i) < 0) {
+        if (pos + i >= L) {  // y[pos+i] out of range
+          index_error = true;
+          break;
+        }
+        if (ys[pos + i] < ys[pos + i - 1]) {
+          index_error = !ks.del(pos - i + 1);
+        } else if (tol < lim) {
+          index_error = !ks.del(pos - i + 1);
+          ++tol;
+        } else {
+          break;
+        }
+      } else if ((pos + i) > L) {
+        if (ys[pos - i] < ys[pos - i + 1]) {
+          index_error = !ks.del(pos - i + 1);
+        } else if (tol < lim) {
+          index_error = !ks.del(pos - i);
+          ++tol;
+        } else {
+          break;
+        }
+      }
+      ++i;
+    }
+  }
+  if (index_error) {  // getGaussianFittings catches IndexError: s10 = s11 = 1e6 (:762-764)
+    if (lane == 0) {
+      a.out[c * 22 + 9] = 1000000.0;
+      a.out[c * 22 + 10] = 1000000.0;
+      a.status[c] |= PFE_ST_DGF_INDEXERROR;
+    }
+    return;
+  }
+  // ---- pass 1 on the compacted kept points, passes 2..8 on all L points
+  GaussAbsBgFn<P> fn;
+  // compaction through LDS: write (x, y) of kept points to rows 0..len-1
+  __shared__ double cx_all[BLOCK / 64][64 * P];
+  double* cx = cx_all[threadIdx.x >> 6];
+  {
+    int rank_base = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const uint64_t wj = ks.w[j];
+      const int i = 64 * j + lane;
+      if ((wj >> lane) & 1ull) {
+        const int r = rank_base + __popcll(wj & ((1ull << lane) - 1ull));
+        cx[r] = (double)i;
+      }
+      rank_base += __popcll(wj);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int m1 = ks.len;
+  double cy[P];
+  bool cok[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int r = lane + 64 * k;
+    cok[k] = r < m1;
+    fn.x[k] = cok[k] ? cx[r] : 0.0;
+    cy[k] = cok[k] ? (double)ys[(int)fn.x[k]] : 0.0;
+    fn.y[k] = cy[k];
+    fn.ok[k] = r < (m1 < 4 ? 4 : m1);  // zero padding to 4 points (:1373-1377)
+  }
+  double p[4], p1[4], p2[4];
+  int nlen = m1;
+  for (int pass = 1; pass <= 8; ++pass) {
+    // initial parameters from the current data (before padding) (:1361-1367)
+    double bvd = -INFINITY;
+    int bid = 1 << 30;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int r = lane + 64 * k;
+      if (r < nlen) {
+        s += fn.y[k];
+        if (bid == (1 << 30) || fn.y[k] > bvd) {
+          bvd = fn.y[k];
+          bid = r;
+        }
+      }
+    }
+    const ArgMax am = wargmax(bvd, bid);
+    const double mean = wsum(s) / (double)nlen;
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (lane + 64 * k < nlen) q += (fn.y[k] - mean) * (fn.y[k] - mean);
+    double xe = 0.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (am.i >> 6 == k) xe = bcast(fn.x[k], am.i & 63);
+    p[0] = sqrt(wsum(q) / (double)nlen);
+    p[1] = xe;
+    p[2] = am.v;
+    p[3] = mean;
+    lmdif<4, P>(fn, p, 200 * 5);
+    const double nfwhm = fabs(FWHM_C * p[0]);
+    // subtraction (:1389-1399; window centred on p[2], the amplitude)
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int i = lane + 64 * k;
+      const double xi = (double)i;
+      const double yi = (double)y[k];
+      double ny = yi;
+      if (ok[k]) {
+        const double ev = g_absbg(xi, p);
+        if (ev <= yi)
+          ny = yi - ev + p[3];
+        else if ((ev > yi) && (xi > (p[2] - (1.5 * nfwhm) / 2.0)) && (xi < (p[2] + (1.5 * nfwhm) / 2.0)))
+          ny = p[3];
+      }
+      fn.x[k] = xi;
+      fn.y[k] = ok[k] ? ny : 0.0;
+      fn.ok[k] = ok[k];
+    }
+    nlen = L;
+    if (pass == 7) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p2[j] = p[j];
+    } else if (pass == 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p1[j] = p[j];
+    }
+  }
+  // ---- final 8-parameter fit on the rotated profile (:1411, :1432-1483)
+  DoubleGaussFn<P> dg;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    dg.x[k] = (double)(lane + 64 * k);
+    dg.y[k] = ok[k] ? (double)y[k] : 0.0;
+    dg.ok[k] = ok[k];
+  }
+  double q8[8] = {p1[0], p1[1], p1[2], p1[3], p2[0], p2[1], p2[2], p2[3]};
+  lmdif<8, P>(dg, q8, 200 * 9);
+  const double f_fwhm1 = fabs(FWHM_C * q8[0]), f_fwhm2 = fabs(FWHM_C * q8[4]);
+  double fchi = 0.0, cchi = 0.0;
+  double ffit[P], cfit[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    ffit[k] = dg.model(q8, k);
+    const double x = dg.x[k];
+    cfit[k] = g_absbg(x, p1) + g_absbg(x, p2) - p1[3] - p2[3] + (p1[3] + p2[3]) / 2.0;
+    if (ok[k]) {
+      if (ffit[k] >= 1.0) fchi += (dg.y[k] - ffit[k]) * (dg.y[k] - ffit[k]) / (double)L;
+      if (cfit[k] >= 1.0) cchi += (dg.y[k] - cfit[k]) * (dg.y[k] - cfit[k]) / (double)L;
+    }
+  }
+  fchi = wsum(fchi);
+  cchi = wsum(cchi);
+  const bool use_final = fchi <= cchi;
+  const double fw1 = use_final ? f_fwhm1 : fabs(FWHM_C * p2[0]);  // combi_fwhm2
+  const double fw2 = use_final ? f_fwhm2 : fabs(FWHM_C * p1[0]);                   // combi_fwhm1
+  const double dchi = use_final ? fchi : cchi;
+  // gf_dgf_std = std(dgf_fit - (gf_fit + minbg - std))  (:755-756)
+  const GaussWS w = a.ws[c];
+  const double t1p[4] = {w.t1[0], w.t1[1], w.t1[2], w.t1[3]};
+  double dd[P];
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const double x = dg.x[k];
+    const double tt = (x - t1p[1]) / fabs(t1p[0]);
+    const double gf = fabs(t1p[2]) * exp(-(tt * tt) / 2.0) + t1p[3];
+    dd[k] = (use_final ? ffit[k] : cfit[k]) - (gf + w.minbg - w.pstd);
+    if (ok[k]) s += dd[k];
+  }
+  const double mu = wsum(s) / (double)L;
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k]) q += (dd[k] - mu) * (dd[k] - mu);
+  const double gstd = fabs(sqrt(wsum(q) / (double)L));
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[9] = (gstd < 3.0) ? o[7] : py_min(fw1, fw2);  // s10 (:758-761)
+    o[10] = dchi;                                   // s11
+  }
+}
+
+// ---- launchers -----------------------------------------------------------------------
+static inline dim3 gw(int64_t n) { return dim3((unsigned)((n + 3) / 4)); }
+
+hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
+  const int L = a.lp;
+#define PFE_GAUSS_LAUNCH(P)                                                             \
+  do {                                                                                  \
+    hipLaunchKernelGGL((k_ghist<P, 4, false>), gw(a.n), dim3(BLOCK), 0, st, a);         \
+    hipLaunchKernelGGL((k_ghist<P, 16, true>), gw(a.n), dim3(BLOCK), 0, st, a);         \
+    hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
+    hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
+  } while (0)
+  if (L <= 64)
+    PFE_GAUSS_LAUNCH(1);
+  else if (L <= 128)
+    PFE_GAUSS_LAUNCH(2);
+  else
+    PFE_GAUSS_LAUNCH(4);
+#undef PFE_GAUSS_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace pfe

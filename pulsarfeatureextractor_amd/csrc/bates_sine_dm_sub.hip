@@ -1,0 +1,501 @@
+// bates_sine_dm_sub.hip — scores 1-4 (sinusoid fits), 12-19 (candidate parameters and
+// DM-curve fit) and 20-22 (sub-band scores) on gfx950, one wavefront per candidate.
+//
+// Reference (PulsarFeatureExtractor/src/):
+//   s1-s4   ProfileOperations.getSinusoidFittings :190-376, fitSine :380-491,
+//           fitSineSqr :495-587;                         PHCXFile.py:454-459
+//   s12-s15 PHCXOperations.getCandidateParameters :81-112; filterScore
+//           CandidateFileInterface.py:84-149;              PHCXFile.py:569-574
+//   s16-s19 PHCXOperations.getDMFittings :121-233;       PHCXFile.py:613-618
+//   s20-s22 PHCXOperations.getSubbandParameters :305-349, getProfileCorr :387-415,
+//           ProfileOperations.getSubband_scores :1585-1686
+#include "bates_common.h"
+
+namespace pfe {
+
+#pragma clang fp contract(off)
+
+// ======================================================================================
+// scores 1-4
+// ======================================================================================
+template <int MPL, bool SQR>
+struct SineFn {
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  double amp, bg;
+  __device__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
+    const double c = TWO_PI * p[0];
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      if (ok[k]) {
+        const double s = sin(c * x[k] + p[1]);
+        if constexpr (!SQR)
+          f[k] = y[k] - (fabs(amp) * s + fabs(bg));               // :418
+        else
+          f[k] = (y[k] - (fabs(amp) * (s * s))) + fabs(bg);      // :522 (sign bug kept)
+      } else {
+        f[k] = 0.0;
+      }
+    }
+  }
+  __device__ double model(const double (&p)[2], int k) const {
+    const double s = sin(TWO_PI * p[0] * x[k] + p[1]);
+    if constexpr (!SQR) return fabs(amp) * s + fabs(bg);          // :425
+    return fabs(amp) * (s * s) + fabs(bg);                        // :529
+  }
+};
+
+// block of 5-zero peak counting (:294-334) on the clipped profile: the zero counter is
+// never reset by a non-zero bin, so a block closes at every 5th zero
+template <int MPL>
+__device__ __forceinline__ int count_peak_blocks(const uint64_t (&nz)[MPL], int len) {
+  int blocks = 0, zeros = 0;
+  bool cur = false;
+#pragma unroll
+  for (int w = 0; w < MPL; ++w) {
+    const uint64_t word = nz[w];
+    const int n = min(64, len - 64 * w);
+    for (int b = 0; b < n; ++b) {
+      if ((word >> b) & 1ull) {
+        cur = true;
+      } else if (zeros < 4) {
+        ++zeros;
+      } else {
+        blocks += cur;
+        cur = false;
+        zeros = 0;
+      }
+    }
+  }
+  return blocks + cur;
+}
+
+template <int MPL, bool SQR>
+__device__ double sine_chisq(const int (&yi)[MPL], int lp, int lane, double amp, int maxima, double y0) {
+  SineFn<MPL, SQR> fn;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    fn.ok[k] = i < lp;
+    fn.x[k] = (double)i;
+    fn.y[k] = (double)yi[k];
+  }
+  fn.amp = amp;
+  fn.bg = amp;
+  double f0, phi0;
+  if constexpr (!SQR) {
+    f0 = (double)maxima / ((double)lp - 1.0);                     // :398
+    if (y0 == amp)
+      phi0 = 0.0;
+    else if (y0 < amp)
+      phi0 = (f0 != 0.0) ? -1.0 / (4.0 * f0) : -1.0 / (4.0 * 0.00000000001);
+    else
+      phi0 = (f0 != 0.0) ? 1.0 / (4.0 * f0) : 1.0 / (4.0 * 0.00000000001);
+  } else {
+    f0 = (double)maxima / ((double)lp - 1.0) / 2.0;               // :535
+    if (y0 == 0.0)
+      phi0 = 0.0;
+    else
+      phi0 = (f0 != 0.0) ? -1.0 / (4.0 * f0) : -1.0 / (4.0 * 0.00000000001);
+  }
+  double p[2] = {f0, phi0};
+  lmdif<2, MPL>(fn, p, 200 * 3);
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (fn.ok[k]) {
+      const double d = fn.y[k] - fn.model(p, k);
+      s += d * d;
+    }
+  return wsum(s) / (double)lp;                                    // :453-458
+}
+
+template <int MPL>
+__global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  const int lane = lane_id();
+  const int lp = a.lp;
+  int v[MPL];
+  load_row_u8<MPL>(a.prof + c * lp, lp, lane, v);
+  const MeanStd ms = int_mean_std<MPL>(v, lp, lane);
+  int vmax = -1, vmin = 1 << 30;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (lane + 64 * k < lp) {
+      vmax = max(vmax, v[k]);
+      vmin = min(vmin, v[k]);
+    }
+  vmax = wmax_i(vmax);
+  vmin = wmin_i(vmin);
+  // s4 = sum((|max-min|/2) - p_i): every partial sum is exact, so = lp*h - sum(p)
+  const double h = (double)abs(vmax - vmin) / 2.0;
+  long long s1 = 0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (lane + 64 * k < lp) s1 += v[k];
+  s1 = wsum_ll(s1);
+  const double s4 = (double)lp * h - (double)s1;
+  // peaks of (p - mean) - std clipped at 0
+  uint64_t nz[MPL];
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const bool pos = (lane + 64 * k < lp) && (((double)v[k] - ms.mean) - ms.std > 0.0);
+    nz[k] = __ballot(pos);
+  }
+  const int maxima = count_peak_blocks<MPL>(nz, lp);
+  const double y0 = (double)__builtin_amdgcn_readfirstlane(v[0]);
+  const double c1 = sine_chisq<MPL, false>(v, lp, lane, h, maxima, y0);
+  const double c2 = sine_chisq<MPL, true>(v, lp, lane, h, maxima, y0);
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[0] = c1 / (double)maxima;                                   // :373 (inf/nan at 0)
+    o[1] = c2 / (double)maxima;                                   // :374
+    o[2] = (double)(maxima > 0 ? maxima - 1 : 0);                 // :376 len(diff)
+    o[3] = s4;
+  }
+}
+
+// ======================================================================================
+// scores 12-19
+// ======================================================================================
+constexpr double KDM = 8.3 * 1000000.0;   // 8.3*10**6 (PHCXOperations.py:187)
+constexpr double DF = 400.0;
+constexpr double F3 = 2593941624.0;       // pow(1374, 3), an exact integer
+
+template <int MPL>
+struct DMFn {
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  double wint, dm, period;
+  __device__ double model(const double (&p)[3], int k) const {
+    const double t = p[1] * KDM * fabs((dm + p[2]) - x[k]) * DF / F3;   // :152
+    const double weff = sqrt(wint + t * t);
+    return p[0] * sqrt((period - weff) / weff);                        // :153
+  }
+  __device__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+};
+
+__device__ __forceinline__ double filter_neg(double v) {
+  // CandidateFileInterface.filterScore(13|14): isEqual(v, 0, 5e-6) == -1 -> 0.0
+  return (fabs(v - 0.0) > 0.000005 && v < 0.0) ? 0.0 : v;
+}
+
+template <int MPL>
+__global__ __launch_bounds__(BLOCK) void k_dmfit(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  const int lane = lane_id();
+  const double* sc = a.scal + c * PFE_NSCAL;
+  const double period = sc[PFE_SCAL_PERIOD_MS], snr = sc[PFE_SCAL_SNR], dm = sc[PFE_SCAL_DM],
+               width = sc[PFE_SCAL_WIDTH], dm_start = sc[PFE_SCAL_DM_START],
+               dm_end = sc[PFE_SCAL_DM_END], length_all = sc[PFE_SCAL_LENGTH_ALL];
+  const int n = a.ndm;
+  DMFn<MPL> fn;
+  const double step = fabs(dm_start - dm_end) / length_all;          // :183
+  const double wint = (width * period) * (width * period);           // :186
+  fn.wint = wint;
+  fn.dm = dm;
+  fn.period = period;
+  double help[MPL];
+  double hmax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    fn.ok[k] = i < n;
+    fn.y[k] = fn.ok[k] ? a.dmcurve[c * n + i] : 0.0;
+    fn.x[k] = dm_start + (double)(128 * i - 1) * step;               // :196 (x = 128k-1)
+    const double t = KDM * fabs(dm - fn.x[k]) * DF / F3;
+    const double weff = sqrt(wint + t * t);                          // :202
+    help[k] = sqrt((period - weff) / weff);                          // :203
+    if (fn.ok[k]) hmax = fmax(hmax, help[k]);
+  }
+  hmax = wmax(hmax);
+  // Python max(): a leading NaN wins, later NaNs are skipped
+  const double h0 = bcast(help[0], 0);
+  if (h0 != h0) hmax = h0;
+  const double amp0 = 255.0 / hmax;                                  // :206-209
+  double p[3] = {amp0, 1.0, 0.0};
+  lmdif<3, MPL>(fn, p, 200 * 4);
+  double chi = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k)
+    if (fn.ok[k]) {
+      const double fit = fn.model(p, k);
+      if (fit >= 1.0) {
+        const double d = fn.y[k] - amp0 * help[k];                   // theo (:206)
+        chi += d * d;
+      }
+    }
+  chi = wsum(chi) / (double)n;                                       // :222-229
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[11] = period;                                                  // s12
+    o[12] = filter_neg(snr);                                         // s13
+    o[13] = filter_neg(dm);                                          // s14
+    o[14] = width;                                                   // s15
+    o[15] = snr / sqrt((period - sqrt(wint)) / sqrt(wint));          // s16 (:191)
+    o[16] = fabs(1.0 - p[1]);                                        // s17
+    o[17] = fabs(p[2]);                                              // s18 (filterScore 18)
+    o[18] = chi;                                                     // s19
+  }
+}
+
+// ======================================================================================
+// scores 20-22
+// ======================================================================================
+// Pearson correlation as numpy.corrcoef computes it:
+//   c_xy = dot(x-mx, y-my) * (1/(N-1)); r = (c_xy / sqrt(c_xx)) / sqrt(c_yy), clipped to [-1,1]
+__device__ __forceinline__ double corr_from(double cxy, double cxx, double cyy) {
+  double r = (cxy / sqrt(cxx)) / sqrt(cyy);
+  if (r > 1.0) r = 1.0;
+  if (r < -1.0) r = -1.0;
+  return r;  // NaN propagates (clip keeps NaN)
+}
+
+// SL = max sub-band length / 64 slots per lane; NSUB <= 16 sub-bands held in registers.
+template <int SL>
+__global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
+  constexpr int NSUB = 16;
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  const int lane = lane_id();
+  const int nsub = a.nsub, lsb = a.lsb;
+  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
+  const int wb = (int)ceil(width * (double)lsb);                     // :1603
+  uint32_t fail = 0;
+  if (wb <= 0 || wb > lsb) fail = PFE_ST_SUBBAND_FAIL;               // m==0 / unbound max_bin
+  if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;                       // corrcoef length mismatch
+  if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
+  if (fail) {
+    if (lane == 0) a.status[c] |= fail;
+    return;
+  }
+  const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
+  const int nw = lsb - wb + 1;                                       // windows per band
+  // boxcar sums: window j of band i = sum_{b<wb} sub[i][j+b] (integers)
+  double bs[NSUB][SL];
+  double max_bin[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    if (i < nsub) {
+      int best = -1, bestj = 0;
+#pragma unroll
+      for (int k = 0; k < SL; ++k) {
+        const int j = lane + 64 * k;
+        int s = 0;
+        if (j < nw)
+          for (int b = 0; b < wb; ++b) s += sb[i * lsb + j + b];
+        bs[i][k] = (double)s;
+        if (j < nw && s > best) {  // first strict max within the lane (j ascending)
+          best = s;
+          bestj = j;
+        }
+      }
+      // first strict maximum over the wave: largest sum, then lowest index
+      int bv = best, bj = (best >= 0) ? bestj : (1 << 30);
+#pragma unroll
+      for (int s = 1; s < 64; s <<= 1) {
+        const int ov = __shfl_xor(bv, s), oj = __shfl_xor(bj, s);
+        if (ov > bv || (ov == bv && oj < bj)) {
+          bv = ov;
+          bj = oj;
+        }
+      }
+      max_bin[i] = (double)(bj + wb / 2);                            // :1628 (Py2 wb/2)
+    } else {
+      max_bin[i] = 0.0;
+#pragma unroll
+      for (int k = 0; k < SL; ++k) bs[i][k] = 0.0;
+    }
+  }
+  // RMS scatter of the maxima (:1633-1659)
+  double msum = 0.0;
+  for (int i = 0; i < nsub; ++i) msum += max_bin[i];
+  const double med = msum / (double)nsub;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i = 0; i < nsub; ++i)
+    if (fabs(max_bin[i] - med) <= (double)wb) {
+      ++count;
+      var_med += (max_bin[i] - med) * (max_bin[i] - med);
+    }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    double mu = 0.0;
+    for (int i = 0; i < nsub; ++i) mu += max_bin[i];
+    mu /= (double)nsub;
+    var = 0.0;
+    for (int i = 0; i < nsub; ++i) var += (max_bin[i] - mu) * (max_bin[i] - mu);
+    var /= (double)(nsub - 1);
+  }
+  const double rms = sqrt(var) / (double)wb;
+  // centre every band's window sums (numpy.cov subtracts the mean first)
+  const double inv = 1.0 / (double)(nw - 1);
+  {
+    double mean[NSUB];
+#pragma unroll
+    for (int i = 0; i < NSUB; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < SL; ++k) s += bs[i][k];
+      mean[i] = s;
+    }
+    wsum_arr(mean);
+#pragma unroll
+    for (int i = 0; i < NSUB; ++i) {
+      const double m = mean[i] / (double)nw;
+#pragma unroll
+      for (int k = 0; k < SL; ++k)
+        if (lane + 64 * k < nw) bs[i][k] = bs[i][k] - m;
+        else bs[i][k] = 0.0;
+    }
+  }
+  double var_i[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) s += bs[i][k] * bs[i][k];
+    var_i[i] = s;
+  }
+  wsum_arr(var_i);
+  // mean pairwise correlation, pairs in the reference's (i<k) order
+  double csum = 0.0;
+  int m = 0;
+#pragma unroll
+  for (int i = 0; i < NSUB - 1; ++i) {
+    if (i + 1 < nsub) {
+      double d[NSUB];
+#pragma unroll
+      for (int k2 = 0; k2 < NSUB; ++k2) {
+        double s = 0.0;
+        if (k2 > i) {
+#pragma unroll
+          for (int k = 0; k < SL; ++k) s += bs[i][k] * bs[k2][k];
+        }
+        d[k2] = s;
+      }
+      wsum_arr(d);
+#pragma unroll
+      for (int k2 = i + 1; k2 < NSUB; ++k2) {
+        if (k2 < nsub) {
+          const double cc = corr_from(d[k2] * inv, var_i[i] * inv, var_i[k2] * inv);
+          if (cc == cc) {
+            csum += cc;
+            ++m;
+          }
+        }
+      }
+    }
+  }
+  if (m == 0) {  // ZeroDivisionError (:1681)
+    if (lane == 0) a.status[c] |= PFE_ST_SUBBAND_FAIL;
+    return;
+  }
+  const double mean_corr = csum / (double)m;
+  // s22: sum of |corr(sub_j, profile)| over values > 0.0055 (:403-415, :345-347)
+  double pv[SL];
+  double pm = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    const int j = lane + 64 * k;
+    pv[k] = (j < lsb) ? (double)a.prof[c * a.lp + j] : 0.0;
+    pm += pv[k];
+  }
+  pm = wsum(pm) / (double)lsb;
+  double pvar = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    if (lane + 64 * k < lsb) pv[k] = pv[k] - pm;
+    else pv[k] = 0.0;
+    pvar += pv[k] * pv[k];
+  }
+  pvar = wsum(pvar);
+  const double inv2 = 1.0 / (double)(lsb - 1);
+  double sv[NSUB], dv[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      s += (j < lsb && i < nsub) ? (double)sb[i * lsb + j] : 0.0;
+    }
+    sv[i] = s;
+  }
+  wsum_arr(sv);
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    const double mu = sv[i] / (double)lsb;
+    double d = 0.0, q = 0.0;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      if (j < lsb && i < nsub) {
+        const double t = (double)sb[i * lsb + j] - mu;
+        d += t * pv[k];
+        q += t * t;
+      }
+    }
+    sv[i] = q;
+    dv[i] = d;
+  }
+  wsum_arr(sv);
+  wsum_arr(dv);
+  double integ = 0.0;
+  for (int i = 0; i < nsub; ++i) {
+    const double cc = fabs(corr_from(dv[i] * inv2, sv[i] * inv2, pvar * inv2));
+    if (cc > 0.0055) integ += cc;
+  }
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[19] = rms;
+    o[20] = mean_corr;
+    o[21] = integ;
+  }
+}
+
+// ---- launchers -----------------------------------------------------------------------
+static inline dim3 grid_waves(int64_t n) { return dim3((unsigned)((n + 3) / 4)); }
+
+hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
+  if (a.lp <= 64)
+    hipLaunchKernelGGL(k_sine<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.lp <= 128)
+    hipLaunchKernelGGL(k_sine<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.lp <= 256)
+    hipLaunchKernelGGL(k_sine<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_sine<16>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
+  if (a.ndm <= 64)
+    hipLaunchKernelGGL(k_dmfit<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.ndm <= 128)
+    hipLaunchKernelGGL(k_dmfit<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.ndm <= 256)
+    hipLaunchKernelGGL(k_dmfit<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_dmfit<16>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
+  if (a.lsb <= 64)
+    hipLaunchKernelGGL(k_subband<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.lsb <= 128)
+    hipLaunchKernelGGL(k_subband<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_subband<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace pfe

@@ -1,0 +1,93 @@
+"""GPU parity of pfe_bates22 (C-ABI) against the reference's golden vectors and the oracle.
+
+Bar (SURVEY.md §8(a) parity classes):
+  * the failing candidates (reference raised -> row dropped) are exactly the same;
+  * s3 (integer peak count), s4, s12-s16, s20, s22: bit-exact on every candidate;
+  * every other score j: the fraction of candidates where GPU and reference differ by more
+    than 1e-5 (and 1e-3) relative is at most 1.5 x the reference's own chaos floor + 3%,
+    where the floor is the fraction of candidates whose score moves when every leastsq
+    start point of the REFERENCE is nudged by one ulp (tests/golden/chaos_floor.json,
+    tools/chaos_floor.py).  For the well-conditioned scores (s1, s2, s19, s21; floor ~0)
+    that means >= 97% within 1e-5; for the ill-conditioned LM outputs (s8, s10, s11, s17,
+    s18: floors 20-60%) the GPU is held to "indistinguishable from a 1-ulp perturbation of
+    the reference".
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, bates_inputs, load
+from oracle.bates import bates22 as oracle_bates22
+from pulsarfeatureextractor_amd.synth import bates_batch
+
+pytestmark = pytest.mark.gpu
+
+BITEXACT = (2, 3, 11, 12, 13, 14, 15, 19, 21)
+FLOOR = json.load(open(os.path.join(GOLDEN, "chaos_floor.json")))
+
+
+def rel_err(got, ref):
+    with np.errstate(all="ignore"):
+        same = (got == ref) | (np.isnan(got) & np.isnan(ref))
+        r = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)
+    r[same] = 0.0
+    r[np.isnan(r)] = np.inf
+    return r
+
+
+def check_against(out, st, ref, ref_ok, tag, floor):
+    gok = (st & 0xFF) == 0
+    assert np.array_equal(gok, ref_ok), f"{tag}: failure pattern differs"
+    got, ref = out[gok], ref[gok]
+    r = rel_err(got, ref)
+    for j in BITEXACT:
+        assert (r[:, j] == 0).all(), f"{tag}: s{j + 1} not bit-exact ({(r[:, j] > 0).sum()} rows)"
+    for j in range(22):
+        if j in BITEXACT:
+            continue
+        for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3")):
+            moved = (r[:, j] > tol).mean()
+            allowed = 1.5 * floor[key][j] + 0.03
+            assert moved <= allowed, (f"{tag}: s{j + 1} differs by > {tol} in {moved:.3f} of rows "
+                                      f"(reference 1-ulp floor {floor[key][j]:.3f})")
+
+
+@pytest.mark.parametrize("name", ["bates22_phcx128", "bates22_superb64"])
+def test_vs_reference_golden(engine, name):
+    d = load(name)
+    prof, sub, curve, scal = bates_inputs(d)
+    out, st = engine.bates22(prof, sub, curve, scal)
+    check_against(out, st, d["out"], d["ok"], name, FLOOR[name])
+
+
+def test_vs_oracle_fresh_inputs(engine):
+    b = bates_batch(160, seed=77)
+    out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    ref, rst = oracle_bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", FLOOR["bates22_phcx128"])
+
+
+def test_device_pointers_and_determinism(engine):
+    import torch
+
+    b = bates_batch(256, seed=5)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in b.items()}
+    o1, s1 = engine.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"])
+    o2, s2 = engine.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"])
+    engine.synchronize()
+    assert torch.equal(s1, s2)
+    assert torch.equal(torch.nan_to_num(o1, 7.0), torch.nan_to_num(o2, 7.0))
+    h, hs = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert np.array_equal(np.nan_to_num(h, nan=7.0), np.nan_to_num(o1.cpu().numpy(), nan=7.0))
+
+
+def test_batch_independence(engine):
+    """A candidate's scores do not depend on its neighbours (shard/concat equivalence)."""
+    b = bates_batch(96, seed=9)
+    full, sf = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    parts = [engine.bates22(b["prof"][i:i + 32], b["sub"][i:i + 32], b["dmcurve"][i:i + 32],
+                            b["scal"][i:i + 32]) for i in range(0, 96, 32)]
+    cat = np.concatenate([p[0] for p in parts])
+    assert np.array_equal(np.nan_to_num(cat, nan=7.0), np.nan_to_num(full, nan=7.0))
