@@ -56,6 +56,9 @@ extern "C" {
 #define PFE_ST_GAUSS_FAIL     0x002u /* scores 5-11 raised           (PHCXFile.py:540-543) */
 #define PFE_ST_DMFIT_FAIL     0x004u /* scores 16-19 raised          (PHCXFile.py:626-629) */
 #define PFE_ST_SUBBAND_FAIL   0x008u /* scores 20-22 raised          (PHCXFile.py:665-668) */
+#define PFE_ST_UNSUPPORTED    0x010u /* outside the shapes this build scores (a histogram with
+                                        more than 1024 Freedman-Diaconis bins, more than 16
+                                        sub-bands); the row is not scored */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu
@@ -75,8 +78,9 @@ void pfe_destroy(pfe_handle* h);
 /* Text of the last error on this handle (or of the last failed pfe_create when h is NULL). */
 const char* pfe_last_error(const pfe_handle* h);
 
-/* Replace the handle's stream (e.g. torch.cuda.current_stream().cuda_stream).  NULL restores
- * the handle's own stream.  The library never destroys a stream it did not create. */
+/* Launch subsequent work on `hip_stream` (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL selects the HIP default (null) stream.  A new handle starts on its own non-blocking
+ * stream.  The library never destroys a stream it did not create. */
 int pfe_set_stream(pfe_handle* h, void* hip_stream);
 /* Block until all work queued on the handle's stream has finished. */
 int pfe_synchronize(pfe_handle* h);
@@ -107,8 +111,8 @@ int pfe_lyon8_f64(pfe_handle* h, const double* prof, int64_t prof_stride, int32_
  *   prof    : n x lp uint8 profile (Profile of the scored section)
  *   sub     : n x nsub x lsb uint8 sub-bands (SubBands of the scored section)
  *   dmcurve : n x ndm fp64 reduced DM curve (PHCXOperations.dm_curve of that section's
- *             DataBlock: max over the first 127 of every 128 values), abscissa
- *             x_k = 128*(k+1) - 129 + 128 = 128k - 1 ... see scal
+ *             DataBlock: max over the first 127 of every 128 values); point k sits at
+ *             DM = dm_start + (128k - 1) * |dm_start - dm_end| / length_all  (:196)
  *   scal    : n x PFE_NSCAL fp64 per-candidate scalars (layout below)
  *   out     : n x 22 fp64 in reference score order (score 1 in column 0)
  *   status  : n x uint32 PFE_ST_* bits (required)

@@ -177,14 +177,16 @@ class Engine:
             raise PfeError(self.lib.pfe_last_error(self._h).decode())
 
     def set_stream(self, stream_handle: int | None):
-        """Launch on an external hipStream_t (e.g. a torch.cuda.Stream's ``cuda_stream``).
+        """Launch on an external hipStream_t (e.g. a torch.cuda.Stream's ``cuda_stream``;
+        0/None is the HIP default stream)."""
+        self._check(self.lib.pfe_set_stream(self._h, stream_handle or None))
 
-        None restores the engine's own stream.  The HIP null stream (handle 0, torch's
-        default stream) cannot be selected: use an explicit stream."""
-        if stream_handle == 0:
-            raise ValueError("set_stream: the null stream (0) cannot be selected; "
-                             "use a torch.cuda.Stream()")
-        self._check(self.lib.pfe_set_stream(self._h, stream_handle))
+    def _follow_torch(self):
+        """Device-tensor calls run on torch's current stream, so they are ordered after the
+        kernels that produced their inputs and before the ones that consume the outputs."""
+        import torch
+
+        self.set_stream(torch.cuda.current_stream().cuda_stream)
 
     def synchronize(self):
         self._check(self.lib.pfe_synchronize(self._h))
@@ -201,6 +203,7 @@ class Engine:
         if dev:
             import torch
 
+            self._follow_torch()
             if out is None:
                 out = torch.empty((n, 8), dtype=torch.float64, device=prof.device)
             dtype_ok = {torch.uint8: "u8", torch.float64: "f64"}
@@ -246,6 +249,7 @@ class Engine:
         if dev:
             import torch
 
+            self._follow_torch()
             if out is None:
                 out = torch.empty((n, 22), dtype=torch.float64, device=prof.device)
             if status is None:

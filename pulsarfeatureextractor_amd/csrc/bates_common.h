@@ -14,7 +14,6 @@ constexpr int BLOCK = 256;                            // 4 waves = 4 candidates 
 
 // internal status bits (not exported)
 constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
-constexpr uint32_t PFE_ST_UNSUPPORTED = 0x010u;
 
 // per-candidate workspace passed between the Gaussian-group kernels
 struct GaussWS {

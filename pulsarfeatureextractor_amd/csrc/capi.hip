@@ -125,7 +125,7 @@ const char* pfe_last_error(const pfe_handle* h) {
 
 int pfe_set_stream(pfe_handle* h, void* s) {
   if (!h) return PFE_EINVAL;
-  h->stream = s ? (hipStream_t)s : h->own;
+  h->stream = (hipStream_t)s;  // NULL selects the HIP default (null) stream
   return PFE_OK;
 }
 
