@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=8000,
                     help="rows for the CPU baseline sample (0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="also time the RCCL all-gather that reassembles the feature matrix")
     return ap.parse_args()
 
 
@@ -194,6 +196,21 @@ def main():
             "avg_kernel_ms_max_over_ranks": kern_ms_max,
         },
     }
+    if args.gather and dist_on:
+        # the optional reassembly step (RCCL all-gather of the n*world x 8 fp64 matrix over
+        # xGMI), timed on its own, outside the headline step
+        from pulsarfeatureextractor_amd.distributed import gather_rows
+
+        gather_rows(out, n * world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        full = gather_rows(out, n * world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gms = (time.perf_counter() - g0) * 1e3
+        result["gather"] = {"ms": gms, "bytes_received_per_rank": int(full.numel() * 8 * (world - 1) / world),
+                            "collective": "all_gather_into_tensor (RCCL)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
     if rank == 0:

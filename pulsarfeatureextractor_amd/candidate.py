@@ -1,0 +1,258 @@
+"""Drop-in mirrors of the reference's per-candidate plug-in API, backed by libpfe.
+
+Reference classes (PulsarFeatureExtractor/src/) and what replaces them here:
+  Candidate               Candidate.py:42-547        -> Candidate (same methods, same dispatch)
+  CandidateFileInterface  CandidateFileInterface.py  -> CandidateFileInterface (filterScore,
+                                                        isEqual, numberOfScores, epsilon)
+  PHCX / SUPERBPHCX       PHCXFile.py, SUPERBPHCXFile.py -> PHCXFile / SUPERBPHCXFile
+  PFD                     PFDFile.py                 -> not in this build
+
+Score values come from the gfx950 kernels through the C-ABI (a batch of one candidate
+here; pulsarfeatureextractor_amd.processor batches whole directories).  As in the reference,
+a candidate whose scoring would have raised raises ``Exception`` with the reference's
+message for that score group.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from . import phcx as _phcx
+from ._native import (PFE_ST_DMFIT_FAIL, PFE_ST_GAUSS_FAIL, PFE_ST_SINE_FAIL,
+                      PFE_ST_SUBBAND_FAIL, Engine)
+
+_engine = None
+_engine_lock = threading.Lock()
+
+
+def get_engine(device: int = 0) -> Engine:
+    """Process-wide default engine (lazily created on `device`)."""
+    global _engine
+    with _engine_lock:
+        if _engine is None:
+            _engine = Engine(device)
+        return _engine
+
+
+def set_engine(engine: Engine) -> None:
+    global _engine
+    with _engine_lock:
+        _engine = engine
+
+
+# status bit -> the exception text the reference raises for that score group
+GROUP_ERRORS = (
+    (PFE_ST_SINE_FAIL, "Sinusoid fitting exception"),          # PHCXFile.py:470
+    (PFE_ST_GAUSS_FAIL, "Gaussian fitting exception"),         # :543
+    (PFE_ST_DMFIT_FAIL, "DM curve fitting exception"),         # :629
+    (PFE_ST_SUBBAND_FAIL, "Subband scoring exception"),        # :668
+    (0x010, "Unsupported candidate shape"),
+)
+
+
+def status_error(st: int) -> str | None:
+    for bit, msg in GROUP_ERRORS:
+        if st & bit:
+            return msg
+    return None
+
+
+class CandidateFileInterface:
+    """CandidateFileInterface.py:38-194 — per-format scorer interface."""
+
+    def __init__(self, debugFlag=False):
+        self.debug = debugFlag
+        self.numberOfScores = 22          # :63
+        self.epsilon = 0.000005           # :64
+
+    def setNumberOfScores(self, n):
+        self.numberOfScores = int(n)
+
+    def filterScore(self, s, value):
+        """:84-112 — scores 13/14 below -epsilon become 0.0; score 18 is made absolute."""
+        if s == 13 or s == 14:
+            return 0.0 if self.isEqual(value, 0.0, self.epsilon) == -1 else value
+        if s == 18:
+            return float(abs(value))
+        return value
+
+    def isEqual(self, a, b, epsln):
+        """:116-149"""
+        if abs(a - b) > epsln:
+            return -1 if a < b else 1
+        return 0
+
+    # abstract API (:153-194)
+    def compute(self):
+        raise NotImplementedError("Please Implement this method")
+
+    def load(self):
+        raise NotImplementedError("Please Implement this method")
+
+    def getProfile(self):
+        raise NotImplementedError("Please Implement this method")
+
+    def isValid(self):
+        raise NotImplementedError("Please Implement this method")
+
+
+class PHCXFile(CandidateFileInterface):
+    """PHCXFile.PHCX (gzip, section 1); SUPERBPHCXFile subclasses with superb=True."""
+
+    SUPERB = False
+
+    def __init__(self, debugFlag, candidateName, engine: Engine | None = None):
+        super().__init__(debugFlag)
+        self.cand = candidateName
+        self.profileIndex = 0 if self.SUPERB else 1
+        self.scores = []
+        self._engine = engine
+        self.setNumberOfScores(22)
+        self.load()
+
+    def load(self):
+        self.data = _phcx.parse(self.cand, superb=self.SUPERB)
+        self.profile = np.asarray(self.data.profile)
+
+    def getprofile(self):
+        return [int(v) for v in self.data.profile]
+
+    def isValid(self):
+        """PHCXFile.isValid (:190-287) on the parsed arrays."""
+        d = self.data
+        nb = 64 if self.SUPERB else 128
+        return (len(d.profile) > 50 and d.subbands.shape == (16, nb) and len(d.dm_curve) > 0)
+
+    @property
+    def engine(self):
+        return self._engine or get_engine()
+
+    def _bates(self):
+        d = self.data
+        out, st = self.engine.bates22(d.profile[None, :].astype(np.uint8),
+                                      d.subbands[None, :, :].astype(np.uint8),
+                                      d.dm_curve[None, :], d.scal[None, :])
+        msg = status_error(int(st[0]))
+        if msg:
+            raise Exception(msg)
+        return [float(v) for v in out[0]]
+
+    def compute(self):
+        """PHCXFile.compute (:383-409): the 22 scores."""
+        self.scores = self._bates()
+        return self.scores
+
+    def computeProfileScores(self):
+        """:291-304 — the profile bins as float scores (--profile)."""
+        self.scores = [float(v) for v in self.data.profile]
+        return self.scores
+
+    def _lyon(self, row):
+        r = np.asarray(row, dtype=np.uint8)[None, :]
+        out = self.engine.lyon8(r, r)
+        return [out[0, 0], out[0, 1], out[0, 2], out[0, 3]]
+
+    def computeProfileStatScores(self):
+        """:320-349 — [mean, std, skew, kurtosis] of the profile."""
+        return self._lyon(self.data.profile)
+
+    def computeDMCurveStatScores(self):
+        """:351-379 — the same statistics of the section-0 DataBlock."""
+        return self._lyon(self.data.lyon_dm)
+
+    def getDMCurveData(self):
+        """:306-318 — the decoded section-0 DataBlock."""
+        return np.asarray(self.data.lyon_dm)
+
+
+class SUPERBPHCXFile(PHCXFile):
+    """SUPERBPHCXFile.SUPERBPHCX: plain XML, section 0, 64-bin (SUPERBPHCXFile.py:80,103)."""
+
+    SUPERB = True
+
+
+class Candidate:
+    """Candidate.py:42-547 with the same methods and file-name dispatch (:136-150)."""
+
+    def __init__(self, name="Unknown", path=""):
+        self.candidateName = name
+        self.candidatePath = path
+        self.scores = []
+        self.label = "Unknown"
+        self.specialScore = -1
+        self.special = "None"
+
+    def _file(self, verbose):
+        if ".pfd" in self.candidateName:
+            raise NotImplementedError("PFD candidates are not supported by this build "
+                                      "(SURVEY.md §8(f) 'next' row)")
+        if ".gz" in self.candidateName:
+            return PHCXFile(verbose, self.candidateName)
+        return SUPERBPHCXFile(verbose, self.candidateName)
+
+    def addScores(self, lineFromFile):
+        for s in lineFromFile.split(","):
+            if s != "" or len(s) != 0:
+                self.scores.append(float(s))
+
+    def calculateScores(self, verbose):
+        self.scores = self._file(verbose).compute()
+        return self.scores
+
+    def calculateProfileScores(self, verbose):
+        self.scores = self._file(verbose).computeProfileScores()
+        return self.scores
+
+    def calculateProfileStatScores(self, verbose):
+        self.scores = self._file(verbose).computeProfileStatScores()
+        return self.scores
+
+    def calculateDMCurveStatScores(self, verbose):
+        self.scores = self._file(verbose).computeDMCurveStatScores()
+        return self.scores
+
+    def getDMCurveData(self, verbose):
+        if ".gz" not in self.candidateName or ".pfd" in self.candidateName:
+            return []
+        self.scores = self._file(verbose).getDMCurveData()
+        return self.scores
+
+    def getScore(self, index):
+        return float(self.scores[index - 1])
+
+    def getName(self):
+        return self.candidateName
+
+    def getPath(self):
+        return self.candidatePath
+
+    def setLabel(self, l):
+        self.label = l
+
+    def getLabel(self):
+        return self.label
+
+    def isPulsar(self):
+        return self.label == "POSITIVE"
+
+    def setSpecialScore(self, special):
+        try:
+            self.specialScore = int(special)
+        except Exception:
+            self.specialScore = -1
+
+    def getSpecialScore(self):
+        return int(self.specialScore)
+
+    def setScores(self, data):
+        self.scores = [float(i) for i in data]
+
+    def setSpecial(self, s):
+        self.special = str(s)
+
+    def getSpecial(self):
+        return str(self.special)
+
+    def __str__(self):
+        return self.candidateName + "," + self.candidatePath

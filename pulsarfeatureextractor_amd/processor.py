@@ -1,0 +1,246 @@
+"""Batched equivalent of the reference's DataProcessor (DataProcessor.py:51-995).
+
+The reference walks a directory and scores one candidate at a time (parse -> score ->
+buffer a text line), catching every exception per candidate
+(DataProcessor.py:491-525, 867-901).  Here the same discovery order, file-type dispatch,
+error log and output text are kept, but candidates are parsed on host worker processes,
+packed into dense arrays and scored in large batches on the GPU through libpfe.
+
+  processPHCXCollectively / processSUPERBCollectively  (:109-146, :451-599)
+  processPHCXSeparately                                (:91-105, :603-687)
+  dmprofPHCX / dmprofSUPERB                            (:255-301, :830-994)
+PFD modes are not part of this build; --label is interactive and out of
+scope.
+"""
+from __future__ import annotations
+
+import datetime
+import fnmatch
+import os
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+from . import phcx as _phcx
+from . import writers
+from .candidate import get_engine, status_error
+
+PHCX_RE = "*.phcx.gz"
+SUPERB_RE = "*.phcx"
+PFD_RES = ("*.pfd", "*.pfd.36scrunch")
+
+
+def discover(directory: str, regexes) -> list[str]:
+    """os.walk + fnmatch in the reference's order (:491-497)."""
+    out = []
+    for ft in regexes:
+        for root, _subs, filenames in os.walk(directory):
+            for fn in fnmatch.filter(filenames, ft):
+                out.append(os.path.join(root, fn))
+    return out
+
+
+def _parse_one(path):
+    try:
+        return _phcx.parse(path), None
+    except Exception as e:  # the reference logs and skips unreadable candidates
+        return None, f"{type(e).__name__}: {e}"
+
+
+def parse_all(paths, workers: int | None = None):
+    if workers is None:
+        workers = min(16, os.cpu_count() or 1)
+    if workers <= 1 or len(paths) < 64:
+        return [_parse_one(p) for p in paths]
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        return list(ex.map(_parse_one, paths, chunksize=64))
+
+
+def _shape_key(c):
+    return (len(c.profile), c.subbands.shape[0], c.subbands.shape[1], len(c.dm_curve))
+
+
+def score_bates(cands, engine=None, batch: int = 1 << 18):
+    """22 scores for parsed candidates: returns (scores (n,22), error message or None)."""
+    engine = engine or get_engine()
+    n = len(cands)
+    out = np.full((n, 22), np.nan)
+    err = [None] * n
+    groups: dict = {}
+    for i, c in enumerate(cands):
+        groups.setdefault(_shape_key(c), []).append(i)
+    for (lp, nsub, lsb, ndm), idx in groups.items():
+        if ndm < 3:  # max() of an empty DM curve / leastsq m < n: the DM fit raises
+            for i in idx:
+                err[i] = "DM curve fitting exception"
+            continue
+        for s in range(0, len(idx), batch):
+            part = idx[s:s + batch]
+            prof = np.stack([cands[i].profile for i in part]).astype(np.uint8)
+            sub = np.stack([cands[i].subbands for i in part]).astype(np.uint8)
+            dmc = np.stack([cands[i].dm_curve for i in part]).astype(np.float64)
+            scal = np.stack([cands[i].scal for i in part]).astype(np.float64)
+            o, st = engine.bates22(prof, sub, dmc, scal)
+            for j, i in enumerate(part):
+                msg = status_error(int(st[j]))
+                if msg:
+                    err[i] = msg
+                else:
+                    out[i] = o[j]
+    return out, err
+
+
+def score_lyon8(cands, engine=None):
+    """8 Lyon features (profile stats + section-0 DataBlock stats) for parsed candidates."""
+    engine = engine or get_engine()
+    n = len(cands)
+    out = np.full((n, 8), np.nan)
+    groups: dict = {}
+    for i, c in enumerate(cands):
+        groups.setdefault((len(c.profile), len(c.lyon_dm)), []).append(i)
+    for (lp, ld), idx in groups.items():
+        prof = np.stack([cands[i].profile for i in idx]).astype(np.uint8)
+        dm = np.stack([cands[i].lyon_dm for i in idx]).astype(np.uint8)
+        out[idx] = engine.lyon8(prof, dm)
+    return out
+
+
+class DataProcessor:
+    """Same entry points and output semantics as DataProcessor.py, batched on the GPU."""
+
+    def __init__(self, debugFlag=False, engine=None, workers=None, log=print):
+        self.debug = debugFlag
+        self.engine = engine
+        self.workers = workers
+        self.log = log
+        self.scoreStore = []
+        self.candidateErrorLog = "CandidateErrorLog.txt"
+        self.superb = False
+        self.phcx = False
+        if not os.path.exists(self.candidateErrorLog):       # :86-87
+            writers.append_text(self.candidateErrorLog, "")
+
+    # ---- discovery ---------------------------------------------------------------
+    def _candidates(self, directory, regexes, single):
+        if directory == "":
+            directory = os.path.dirname(os.path.realpath(__file__))
+        if not single:
+            return discover(directory, regexes)
+        if ".txt" in directory:  # a list of candidate paths (the reference reads self.path)
+            with open(directory) as f:
+                return [ln.strip() for ln in f if ln.strip()]
+        return [directory]
+
+    def _fail(self, cand, why):
+        self.log(f"Error reading profile data :\n\t{why}\n{cand}  did not have scores generated.")
+        writers.append_text(self.candidateErrorLog, cand + "\n")
+
+    def _finish(self, outPath, processed, ok, failed, start):
+        end = datetime.datetime.now()
+        writers.append_text(outPath, "".join(s + "\n" for s in self.scoreStore))
+        self.log(f"\nCandidates processed:\t{processed}\nSuccesses:\t{ok}\nFailures:\t{failed}\n"
+                 f"Execution time:  {end - start}")
+
+    # ---- 22 scores / profile bins ---------------------------------------------------
+    def processCollectively(self, directory, verbose, regexes, outPath, arff, genProfileData,
+                            single):
+        if arff:
+            nattr = 22
+            if genProfileData:
+                nattr = 64 if self.superb else 128
+            writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
+        start = datetime.datetime.now()
+        paths = self._candidates(directory, regexes, single)
+        parsed = parse_all(paths, self.workers)
+        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
+        cands = [parsed[i][0] for i in good]
+        if genProfileData:
+            scores = [[float(v) for v in c.profile] for c in cands]
+            errs = [None] * len(cands)
+        else:
+            sc, errs = score_bates(cands, self.engine)
+            scores = [sc[j] for j in range(len(cands))]
+        res = {i: (scores[j], errs[j]) for j, i in enumerate(good)}
+        ok = failed = 0
+        for i, p in enumerate(paths):
+            if i not in res:
+                self._fail(p, parsed[i][1])
+                failed += 1
+                continue
+            s, e = res[i]
+            if e:
+                self._fail(p, e)
+                failed += 1
+                continue
+            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
+            ok += 1
+        self._finish(outPath, len(paths), ok, failed, start)
+
+    def processPHCXCollectively(self, directory, verbose, outPath, arff, genProfileData,
+                                processSingleCandidate):
+        self.phcx = True
+        self.processCollectively(directory, verbose, [PHCX_RE], outPath, arff, genProfileData,
+                                 processSingleCandidate)
+
+    def processSUPERBCollectively(self, directory, verbose, outPath, arff, genProfileData,
+                                  processSingleCandidate):
+        self.superb = True
+        self.processCollectively(directory, verbose, [SUPERB_RE], outPath, arff, genProfileData,
+                                 processSingleCandidate)
+
+    def processSeparately(self, directory, verbose, regexes, single):
+        paths = self._candidates(directory, regexes, single)
+        parsed = parse_all(paths, self.workers)
+        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
+        sc, errs = score_bates([parsed[i][0] for i in good], self.engine)
+        for j, i in enumerate(good):
+            if errs[j]:
+                self._fail(paths[i], errs[j])
+            else:
+                with open(paths[i] + ".dat", "w") as f:                 # :442-447
+                    f.write(writers.dat_text(sc[j]))
+        for i, (c, e) in enumerate(parsed):
+            if c is None:
+                self._fail(paths[i], e)
+
+    def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
+        self.phcx = True
+        self.processSeparately(directory, verbose, [PHCX_RE], processSingleCandidate)
+
+    # ---- 8 Lyon features -------------------------------------------------------------
+    def dmprof(self, directory, verbose, regexes, outPath, arff, single):
+        if arff:
+            writers.write_arff_header(outPath, writers.arff_header("dmprof"))
+        start = datetime.datetime.now()
+        paths = self._candidates(directory, regexes, single)
+        parsed = parse_all(paths, self.workers)
+        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
+        feats = score_lyon8([parsed[i][0] for i in good], self.engine)
+        row = {i: feats[j] for j, i in enumerate(good)}
+        ok = failed = 0
+        for i, p in enumerate(paths):
+            if i not in row:
+                self._fail(p, parsed[i][1])
+                failed += 1
+                continue
+            s = row[i]
+            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
+            ok += 1
+        self._finish(outPath, len(paths), ok, failed, start)
+
+    def dmprofPHCX(self, directory, verbose, outPath, arff, processSingleCandidate):
+        self.phcx = True
+        self.dmprof(directory, verbose, [PHCX_RE], outPath, arff, processSingleCandidate)
+
+    def dmprofSUPERB(self, directory, verbose, outPath, arff, processSingleCandidate):
+        self.superb = True
+        self.dmprof(directory, verbose, [SUPERB_RE], outPath, arff, processSingleCandidate)
+
+    # ---- not in this build -------------------------------------------------------------
+    def _pfd(self, *a, **k):
+        raise NotImplementedError("PFD candidates are not supported by this build "
+                                  "(SURVEY.md §8(f) 'next' row)")
+
+    processPFDSeparately = processPFDCollectively = dmprofPFD = _pfd
+    processPFDAndPHCXSeparately = processPFDAndPHCXCollectively = _pfd
+    labelPHCX = labelPFD = _pfd
