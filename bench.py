@@ -190,7 +190,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "pfe::lyon8_u8_fast<128>",
+            "kernel": "pfe::lyon8_u8_fast3<128, 2>",
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "avg_kernel_ms": kern_ms,
             "avg_kernel_ms_max_over_ranks": kern_ms_max,

@@ -26,6 +26,8 @@
 //   * Generic path (any lengths/alignment): one wave per (candidate,row), byte loads,
 //     64-bit per-lane sums, 128-bit finalisation.
 
+#include <cstdlib>
+
 #include "pfe_common.h"
 
 namespace pfe {
@@ -206,6 +208,220 @@ __global__ __launch_bounds__(256) void lyon8_u8_fast(const uint8_t* __restrict__
   }
 }
 
+// ---- fast path, v2 -------------------------------------------------------------------
+// Same lane mapping as lyon8_u8_fast; per 4 bytes: S1 = sum x and S2 = sum x^2 by unsigned
+// v_dot4 (no XOR), the shifted y = x-128 only for y^3/y^4 (v_perm unpack, packed i16
+// sub/mul, v_dot2); branch-free finalisation with compile-time powers of 1/L (exact for
+// L = 2^k, so mean and m2..m4 are the correctly rounded rationals with no division); the
+// next iteration's four dwordx4 loads are issued before the current one is reduced.
+struct Acc2 {
+  uint32_t s1, s2;
+  int t3;
+  uint64_t t4;
+};
+
+__device__ __forceinline__ void acc2_dword(uint32_t x, Acc2& a, uint32_t& t4a) {
+  a.s1 = __builtin_amdgcn_udot4(x, 0x01010101u, a.s1, false);
+  a.s2 = __builtin_amdgcn_udot4(x, x, a.s2, false);
+  const uint32_t lo = __builtin_amdgcn_perm(0u, x, 0x0c020c00u);  // [b0,0,b2,0]
+  const uint32_t hi = __builtin_amdgcn_perm(0u, x, 0x0c030c01u);  // [b1,0,b3,0]
+  short2v ylo = __builtin_bit_cast(short2v, lo) - (short2v){128, 128};
+  short2v yhi = __builtin_bit_cast(short2v, hi) - (short2v){128, 128};
+  ushort2v qlo = __builtin_bit_cast(ushort2v, ylo) * __builtin_bit_cast(ushort2v, ylo);
+  ushort2v qhi = __builtin_bit_cast(ushort2v, yhi) * __builtin_bit_cast(ushort2v, yhi);
+  a.t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qlo), ylo, a.t3, false);
+  a.t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qhi), yhi, a.t3, false);
+  t4a = __builtin_amdgcn_udot2(qlo, qlo, t4a, false);
+  t4a = __builtin_amdgcn_udot2(qhi, qhi, t4a, false);
+}
+
+__device__ __forceinline__ void acc2_x4(const u32x4 q, Acc2& a) {
+  uint32_t u = 0, v = 0;  // each <= 2 dwords * 4 * 2^28 = 2^31
+  acc2_dword(q.x, a, u);
+  acc2_dword(q.y, a, u);
+  acc2_dword(q.z, a, v);
+  acc2_dword(q.w, a, v);
+  a.t4 += (uint64_t)u + (uint64_t)v;
+}
+
+template <int G>
+__device__ __forceinline__ void acc2_reduce(Acc2& a) {
+  a.s1 = (uint32_t)group_sum_i32<G>((int)a.s1);
+  a.s2 = (uint32_t)group_sum_i32<G>((int)a.s2);
+  a.t3 = group_sum_i32<G>(a.t3);
+  a.t4 = group_sum_u64<G>(a.t4);
+}
+
+// the four statistics of one row from its exact sums; n = L (a power of two)
+template <int L>
+__device__ __forceinline__ void stats4(const Acc2& a, double (&st)[4]) {
+  constexpr double IN1 = 1.0 / L, IN2 = IN1 * IN1, IN3 = IN2 * IN1, IN4 = IN2 * IN2;
+  const long long S1 = (long long)a.s1;
+  const long long T1 = S1 - 128ll * L;                                    // sum y
+  const long long T2 = (long long)a.s2 - 256ll * S1 + 16384ll * L;         // sum y^2
+  const long long T3 = a.t3;
+  typedef unsigned long long u64;
+  const long long N2 = (long long)L * T2 - T1 * T1;
+  const long long T1s = T1 * T1;
+  const long long N3 = (long long)L * L * T3 - 3ll * L * T1 * T2 + 2ll * T1s * T1;
+  const u64 N4 = (u64)L * L * L * a.t4 - 4ull * (u64)L * L * (u64)(T1 * T3) +
+                 6ull * (u64)L * (u64)(T1s * T2) - 3ull * (u64)T1s * (u64)T1s;
+  const double mean = (double)S1 * IN1;
+  const double m2 = (double)N2 * IN2;
+  const double m3 = (double)N3 * IN3;
+  const double m4 = (double)N4 * IN4;
+  const double sd = sqrt(m2);
+  const double e = 2.220446049250313e-16 * mean;
+  const bool zero = m2 <= e * e;                                          // scipy's rule
+  st[0] = mean;
+  st[1] = sd;
+  st[2] = zero ? __builtin_nan("") : m3 / (m2 * sd);
+  st[3] = zero ? __builtin_nan("") : m4 / (m2 * m2) - 3.0;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void lyon8_u8_fast2(const uint8_t* __restrict__ prof,
+                                                      int64_t ps,
+                                                      const uint8_t* __restrict__ dm,
+                                                      int64_t ds, int64_t n,
+                                                      double* __restrict__ out) {
+  constexpr int LPC = L / 32;
+  constexpr int CPW = 64 / LPC;
+  constexpr int SPL = 8 / LPC;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPC;
+  const int cw = lane / LPC;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * CPW;
+  auto load = [&](int64_t c, u32x4& p0, u32x4& p1, u32x4& d0, u32x4& d1) {
+    if (c < n) {
+      const u32x4* pp = reinterpret_cast<const u32x4*>(prof + c * ps + sub * 32);
+      const u32x4* dp = reinterpret_cast<const u32x4*>(dm + c * ds + sub * 32);
+      p0 = __builtin_nontemporal_load(pp);
+      p1 = __builtin_nontemporal_load(pp + 1);
+      d0 = __builtin_nontemporal_load(dp);
+      d1 = __builtin_nontemporal_load(dp + 1);
+    } else {
+      p0 = p1 = d0 = d1 = (u32x4){0, 0, 0, 0};
+    }
+  };
+  int64_t base = wave * CPW;
+  u32x4 p0, p1, d0, d1;
+  load(base + cw, p0, p1, d0, d1);
+  for (; base < n; base += stride) {
+    const int64_t c = base + cw;
+    u32x4 q0, q1, e0, e1;
+    load(c + stride, q0, q1, e0, e1);  // prefetch the next candidate of this lane group
+    Acc2 sp = {0, 0, 0, 0}, sd = {0, 0, 0, 0};
+    acc2_x4(p0, sp);
+    acc2_x4(p1, sp);
+    acc2_x4(d0, sd);
+    acc2_x4(d1, sd);
+    acc2_reduce<LPC>(sp);
+    acc2_reduce<LPC>(sd);
+    const int j0 = sub * SPL;
+    const bool is_dm = j0 >= 4;
+    Acc2 s;
+    s.s1 = is_dm ? sd.s1 : sp.s1;
+    s.s2 = is_dm ? sd.s2 : sp.s2;
+    s.t3 = is_dm ? sd.t3 : sp.t3;
+    s.t4 = is_dm ? sd.t4 : sp.t4;
+    double st[4];
+    stats4<L>(s, st);
+    if (c < n) {
+      double* o = out + c * 8 + j0;
+      if constexpr (SPL == 4) {
+        __builtin_nontemporal_store((f64x2){st[0], st[1]}, reinterpret_cast<f64x2*>(o));
+        __builtin_nontemporal_store((f64x2){st[2], st[3]}, reinterpret_cast<f64x2*>(o) + 1);
+      } else if constexpr (SPL == 2) {
+        const bool hi2 = (j0 & 3) != 0;
+        __builtin_nontemporal_store((f64x2){hi2 ? st[2] : st[0], hi2 ? st[3] : st[1]},
+                                    reinterpret_cast<f64x2*>(o));
+      } else {
+        const int k = j0 & 3;
+        const double v = k == 0 ? st[0] : k == 1 ? st[1] : k == 2 ? st[2] : st[3];
+        __builtin_nontemporal_store(v, o);
+      }
+    }
+    p0 = q0;
+    p1 = q1;
+    d0 = e0;
+    d1 = e1;
+  }
+}
+
+// ---- fast path, v3 -------------------------------------------------------------------
+// v2's arithmetic, but each wave step covers U consecutive groups of CPW candidates, so a
+// wave reads U*CPW*L contiguous bytes of each input in one burst (8 KiB per array at
+// L = 128, U = 4: measured +5% HBM throughput over one group, tools/membw.hip), and all
+// 4*U dwordx4 loads are issued unconditionally (out-of-range groups re-read the last row)
+// before any is consumed, so the compiler's vmcnt counting keeps them all in flight.
+template <int L, int U>
+__global__ __launch_bounds__(256) void lyon8_u8_fast3(const uint8_t* __restrict__ prof,
+                                                      int64_t ps,
+                                                      const uint8_t* __restrict__ dm,
+                                                      int64_t ds, int64_t n,
+                                                      double* __restrict__ out) {
+  constexpr int LPC = L / 32;
+  constexpr int CPW = 64 / LPC;
+  constexpr int SPL = 8 / LPC;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPC;
+  const int cw = lane / LPC;
+  const int j0 = sub * SPL;
+  const bool is_dm = j0 >= 4;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t step = (int64_t)CPW * U;
+  const int64_t stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * step;
+  for (int64_t base = wave * step; base < n; base += stride) {
+    u32x4 p[U][2], d[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t c = base + u * CPW + cw;
+      c = c < n ? c : n - 1;
+      const u32x4* pp = reinterpret_cast<const u32x4*>(prof + c * ps + sub * 32);
+      const u32x4* dp = reinterpret_cast<const u32x4*>(dm + c * ds + sub * 32);
+      p[u][0] = __builtin_nontemporal_load(pp);
+      p[u][1] = __builtin_nontemporal_load(pp + 1);
+      d[u][0] = __builtin_nontemporal_load(dp);
+      d[u][1] = __builtin_nontemporal_load(dp + 1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = base + u * CPW + cw;
+      Acc2 sp = {0, 0, 0, 0}, sd = {0, 0, 0, 0};
+      acc2_x4(p[u][0], sp);
+      acc2_x4(p[u][1], sp);
+      acc2_x4(d[u][0], sd);
+      acc2_x4(d[u][1], sd);
+      acc2_reduce<LPC>(sp);
+      acc2_reduce<LPC>(sd);
+      Acc2 s;
+      s.s1 = is_dm ? sd.s1 : sp.s1;
+      s.s2 = is_dm ? sd.s2 : sp.s2;
+      s.t3 = is_dm ? sd.t3 : sp.t3;
+      s.t4 = is_dm ? sd.t4 : sp.t4;
+      double st[4];
+      stats4<L>(s, st);
+      if (c < n) {
+        double* o = out + c * 8 + j0;
+        if constexpr (SPL == 4) {
+          __builtin_nontemporal_store((f64x2){st[0], st[1]}, reinterpret_cast<f64x2*>(o));
+          __builtin_nontemporal_store((f64x2){st[2], st[3]}, reinterpret_cast<f64x2*>(o) + 1);
+        } else if constexpr (SPL == 2) {
+          const bool hi2 = (j0 & 3) != 0;
+          __builtin_nontemporal_store((f64x2){hi2 ? st[2] : st[0], hi2 ? st[3] : st[1]},
+                                      reinterpret_cast<f64x2*>(o));
+        } else {
+          const int k = j0 & 3;
+          const double v = k == 0 ? st[0] : k == 1 ? st[1] : k == 2 ? st[2] : st[3];
+          __builtin_nontemporal_store(v, o);
+        }
+      }
+    }
+  }
+}
+
 // ---- generic path ----------------------------------------------------------------------
 // One wave per (candidate,row).  Rows of any length/alignment.
 __global__ __launch_bounds__(256) void lyon8_u8_generic(const uint8_t* __restrict__ prof,
@@ -303,7 +519,43 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
   if (n <= 0) return hipSuccess;
   const bool aligned = ((uintptr_t)prof % 16 == 0) && ((uintptr_t)dm % 16 == 0) &&
                        (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
+  static const int variant = [] {
+    const char* v = getenv("PFE_LYON8_VARIANT");  // A/B switch for benchmarking only
+    return v ? atoi(v) : 32;
+  }();
+  if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256) && variant >= 31) {
+    const int U = variant - 30;  // 31 -> U=1, 32 -> U=2, 34 -> U=4
+    const int cpw = 64 / (lp / 32) * U;
+    const int grid = grid_for((n + cpw - 1) / cpw);
+#define PFE_L8(LL, UU) \
+  hipLaunchKernelGGL((lyon8_u8_fast3<LL, UU>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out)
+#define PFE_L8U(LL)          \
+  do {                       \
+    if (U == 1)              \
+      PFE_L8(LL, 1);         \
+    else if (U == 2)         \
+      PFE_L8(LL, 2);         \
+    else                     \
+      PFE_L8(LL, 4);         \
+  } while (0)
+    if (lp == 64)
+      PFE_L8U(64);
+    else if (lp == 128)
+      PFE_L8U(128);
+    else
+      PFE_L8U(256);
+#undef PFE_L8U
+#undef PFE_L8
+  } else if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256) && variant == 2) {
+    const int cpw = 64 / (lp / 32);
+    const int grid = grid_for((n + cpw - 1) / cpw);
+    if (lp == 64)
+      hipLaunchKernelGGL(lyon8_u8_fast2<64>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+    else if (lp == 128)
+      hipLaunchKernelGGL(lyon8_u8_fast2<128>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+    else
+      hipLaunchKernelGGL(lyon8_u8_fast2<256>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
+  } else if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
     const int cpw = 64 / (lp / 32);
     const int grid = grid_for((n + cpw - 1) / cpw);
     if (lp == 64)
