@@ -10,7 +10,11 @@ namespace pfe {
 
 constexpr double TWO_PI = 6.283185307179586;          // Python's 2*pi (numpy.pi * 2)
 constexpr double FWHM_C = 2.3548200450309493;         // 2*sqrt(2*log(2)) as numpy computes it
-constexpr int BLOCK = 256;                            // 4 waves = 4 candidates per block
+// One wave (= one candidate) per workgroup: the fit lengths are heavy-tailed (median ~200,
+// p90 ~900 function evaluations for the 8-parameter fit), and a multi-wave workgroup holds
+// its CU slots until its slowest wave retires.
+constexpr int BLOCK = 64;
+constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
 // internal status bits (not exported)
 constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
@@ -22,6 +26,7 @@ struct GaussWS {
   double pstd;      // profile.std()
   double t1[4];     // fitGaussianT1 parameters (sigma, mu, A, bg)       (:739, :1246)
   double pad;
+  double dg[8];     // store_p1 ++ store_p2 of fitDoubleGaussian's passes 8 and 7 (:1402-1408)
 };
 
 struct BatesArgs {
@@ -39,6 +44,10 @@ struct BatesArgs {
   double c_lp;       // pow(lp, -0.3333333)     (ProfileOperationsInterface.py:151)
   double c_lp1;      // pow(lp-1, -0.3333333)
 };
+
+static inline dim3 grid_for_candidates(int64_t n) {
+  return dim3((unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
+}
 
 __device__ __forceinline__ int64_t wave_candidate() {
   return ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;

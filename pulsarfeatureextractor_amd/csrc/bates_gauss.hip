@@ -101,11 +101,11 @@ template <int MPL>
 struct GaussFn {  // y - |A| exp(-((x-mu)/sigma)^2 / 2)
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ double model(const double (&p)[3], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[3], int k) const {
     const double t = (x[k] - p[1]) / p[0];
     return fabs(p[2]) * exp(-(t * t) / 2.0);
   }
-  __device__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
@@ -116,11 +116,11 @@ struct GaussFixedFn {  // mu fixed at xmax; parameters (sigma, A)
   double x[MPL], y[MPL];
   bool ok[MPL];
   double xmax;
-  __device__ double model(const double (&p)[2], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[2], int k) const {
     const double t = (x[k] - xmax) / p[0];
     return fabs(p[1]) * exp(-(t * t) / 2.0);
   }
-  __device__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
@@ -372,11 +372,11 @@ template <int MPL>
 struct GaussBgFn {  // y - (|A| exp(-((x-mu)/|sigma|)^2/2) + bg)      (:1226)
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ double model(const double (&p)[4], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[4], int k) const {
     const double t = (x[k] - p[1]) / fabs(p[0]);
     return fabs(p[2]) * exp(-(t * t) / 2.0) + p[3];
   }
-  __device__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
@@ -452,7 +452,7 @@ template <int MPL>
 struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
       if (ok[k]) {
@@ -473,13 +473,13 @@ template <int MPL>
 struct DoubleGaussFn {  // :1459-1460
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ double model(const double (&p)[8], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[8], int k) const {
     const double t1 = (x[k] - p[1]) / fabs(p[0]);
     const double t2 = (x[k] - p[5]) / fabs(p[4]);
     return (fabs(p[2]) * exp(-(t1 * t1) / 2.0)) + (fabs(p[6]) * exp(-(t2 * t2) / 2.0)) +
            (fabs(p[3]) + fabs(p[7])) / 2.0;
   }
-  __device__ void operator()(const double (&p)[8], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[8], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
@@ -706,13 +706,42 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
       for (int j = 0; j < 4; ++j) p1[j] = p[j];
     }
   }
-  // ---- final 8-parameter fit on the rotated profile (:1411, :1432-1483)
+  if (lane == 0) {
+    GaussWS* wp = a.ws + c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wp->dg[j] = p1[j];
+      wp->dg[4 + j] = p2[j];
+    }
+  }
+}
+
+// final 8-parameter fit (:1411, :1432-1483), the combination rule (:1413-1428) and the
+// s10/s11 selection of getGaussianFittings (:747-768)
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) return;
+  const int lane = lane_id();
+  const int L = a.lp;
+  const int cut = L / 2;
+  const GaussWS w = a.ws[c];
+  bool ok[P];
   DoubleGaussFn<P> dg;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    dg.x[k] = (double)(lane + 64 * k);
-    dg.y[k] = ok[k] ? (double)y[k] : 0.0;
+    const int i = lane + 64 * k;
+    ok[k] = i < L;
+    dg.x[k] = (double)i;
+    dg.y[k] = ok[k] ? (double)a.prof[c * L + (i + cut) % L] : 0.0;
     dg.ok[k] = ok[k];
+  }
+  double p1[4], p2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p1[j] = w.dg[j];
+    p2[j] = w.dg[4 + j];
   }
   double q8[8] = {p1[0], p1[1], p1[2], p1[3], p2[0], p2[1], p2[2], p2[3]};
   lmdif<8, P>(dg, q8, 200 * 9);
@@ -736,7 +765,6 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
   const double fw2 = use_final ? f_fwhm2 : fabs(FWHM_C * p1[0]);                   // combi_fwhm1
   const double dchi = use_final ? fchi : cchi;
   // gf_dgf_std = std(dgf_fit - (gf_fit + minbg - std))  (:755-756)
-  const GaussWS w = a.ws[c];
   const double t1p[4] = {w.t1[0], w.t1[1], w.t1[2], w.t1[3]};
   double dd[P];
   double s = 0.0;
@@ -762,7 +790,7 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
 }
 
 // ---- launchers -----------------------------------------------------------------------
-static inline dim3 gw(int64_t n) { return dim3((unsigned)((n + 3) / 4)); }
+static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }
 
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const int L = a.lp;
@@ -772,6 +800,7 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_ghist<P, 16, true>), gw(a.n), dim3(BLOCK), 0, st, a);         \
     hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
     hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
+    hipLaunchKernelGGL((k_gdg8<P>), gw(a.n), dim3(BLOCK), 0, st, a);                    \
   } while (0)
   if (L <= 64)
     PFE_GAUSS_LAUNCH(1);

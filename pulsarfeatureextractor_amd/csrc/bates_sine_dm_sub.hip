@@ -23,7 +23,7 @@ struct SineFn {
   double x[MPL], y[MPL];
   bool ok[MPL];
   double amp, bg;
-  __device__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
     const double c = TWO_PI * p[0];
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
@@ -38,7 +38,7 @@ struct SineFn {
       }
     }
   }
-  __device__ double model(const double (&p)[2], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[2], int k) const {
     const double s = sin(TWO_PI * p[0] * x[k] + p[1]);
     if constexpr (!SQR) return fabs(amp) * s + fabs(bg);          // :425
     return fabs(amp) * (s * s) + fabs(bg);                        // :529
@@ -168,12 +168,12 @@ struct DMFn {
   double x[MPL], y[MPL];
   bool ok[MPL];
   double wint, dm, period;
-  __device__ double model(const double (&p)[3], int k) const {
+  __device__ __forceinline__ double model(const double (&p)[3], int k) const {
     const double t = p[1] * KDM * fabs((dm + p[2]) - x[k]) * DF / F3;   // :152
     const double weff = sqrt(wint + t * t);
     return p[0] * sqrt((period - weff) / weff);                        // :153
   }
-  __device__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
+  __device__ __forceinline__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
 }
 
 // ---- launchers -----------------------------------------------------------------------
-static inline dim3 grid_waves(int64_t n) { return dim3((unsigned)((n + 3) / 4)); }
+static inline dim3 grid_waves(int64_t n) { return grid_for_candidates(n); }
 
 hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
   if (a.lp <= 64)

@@ -82,7 +82,7 @@ __device__ __forceinline__ bool row_ge(int lane, int k, int j) { return k > 0 ||
 
 // ---- qrfac (pivot = true) on the distributed m x N matrix a -------------------------------
 template <int N, int MPL>
-__device__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N], double (&acnorm)[N]) {
+__device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N], double (&acnorm)[N]) {
   const int lane = lane_id();
   double wa[N];
   {
@@ -360,7 +360,7 @@ struct LMResult {
 };
 
 template <int N, int MPL, class Fn>
-__device__ LMResult lmdif(const Fn& fcn, double (&x)[N], int maxfev) {
+__device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int maxfev) {
   const double eps = 1.4901161193847656e-08;  // sqrt(max(epsfcn, epsmch)) = 2^-26
   double fvec[MPL], wa4[MPL];
   double fjac[MPL][N];

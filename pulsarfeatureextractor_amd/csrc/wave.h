@@ -112,19 +112,27 @@ __device__ __forceinline__ int wscan_excl(int v) {
   return x - v;
 }
 
+// Value the optimiser cannot see through: keeps a select chain over register-array elements
+// from being folded back into a load through a runtime index (which would demote the whole
+// array to scratch memory).
+template <typename T>
+__device__ __forceinline__ T opaque(T v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
 // select arr[idx] for a small uniform runtime idx without dynamic register indexing
 template <int N, typename T>
 __device__ __forceinline__ T sel(const T (&a)[N], int idx) {
-  T r = a[0];
+  T r = opaque(a[0]);
 #pragma unroll
-  for (int k = 1; k < N; ++k) r = (idx == k) ? a[k] : r;
+  for (int k = 1; k < N; ++k) r = (idx == k) ? opaque(a[k]) : r;
   return r;
 }
 template <int N, typename T>
 __device__ __forceinline__ void put(T (&a)[N], int idx, T v) {
 #pragma unroll
-  for (int k = 0; k < N; ++k)
-    if (idx == k) a[k] = v;
+  for (int k = 0; k < N; ++k) a[k] = (idx == k) ? v : opaque(a[k]);
 }
 
 }  // namespace pfe
