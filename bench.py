@@ -42,12 +42,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=10_000_000, help="candidates per GPU")
+    ap.add_argument("--n", type=int, default=None,
+                    help="candidates per GPU (default 10M for lyon8, 1M for bates22)")
     ap.add_argument("--lp", type=int, default=128)
     ap.add_argument("--ld", type=int, default=128)
     ap.add_argument("--path", choices=["lyon8", "bates22"], default="lyon8")
-    ap.add_argument("--cpu-sample", type=int, default=8000,
-                    help="rows for the CPU baseline sample (0 disables)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL all-gather that reassembles the feature matrix")
@@ -93,8 +94,45 @@ def cpu_baseline_lyon8(lp, ld, sample):
     }
 
 
+def cpu_baseline_bates22(lp, sample):
+    import warnings
+
+    from oracle.bates import bates22
+    from pulsarfeatureextractor_amd.synth import bates_batch
+
+    b = bates_batch(sample, lp=lp, lsb=lp, seed=4243)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        bates22(b["prof"][:5], b["sub"][:5], b["dmcurve"][:5], b["scal"][:5])
+        t0 = time.perf_counter()
+        bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+        dt = time.perf_counter() - t0
+    return {
+        "value": sample / dt,
+        "unit": "candidates/sec",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{sample} synthetic config-3 candidates ({lp}-bin profile, 16x{lp} sub-bands, "
+                  f"128-point DM curve) through the reference-equivalent numpy/scipy.optimize."
+                  f"leastsq restatement (oracle.bates.bates22), {dt:.1f} s on 1 host core",
+    }
+
+
+def load_ops_per_candidate():
+    p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["ops_per_candidate"]
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
+    if args.n is None:
+        args.n = 10_000_000 if args.path == "lyon8" else 1_000_000
+    if args.cpu_sample is None:
+        args.cpu_sample = 8000 if args.path == "lyon8" else 300
     import torch
     import torch.distributed as dist
 
@@ -118,21 +156,38 @@ def main():
     eng.set_stream(stream.cuda_stream)
 
     n = args.n
-    if args.path != "lyon8":
-        raise SystemExit("bench.py: only the lyon8 headline path is benchmarked in this round")
-    # rank-specific synthetic shard, resident in HBM before timing
-    prof, dm = lyon_batch_torch(n, args.lp, args.ld, seed=20261017 + rank, device=f"cuda:{local}")
-    out = torch.empty((n, 8), dtype=torch.float64, device=f"cuda:{local}")
-    torch.cuda.synchronize()
+    dev = f"cuda:{local}"
+    if args.path == "lyon8":
+        # rank-specific synthetic shard, resident in HBM before timing
+        prof, dm = lyon_batch_torch(n, args.lp, args.ld, seed=20261017 + rank, device=dev)
+        out = torch.empty((n, 8), dtype=torch.float64, device=dev)
 
-    def step():
-        eng.lyon8(prof, dm, out=out)
+        def step():
+            eng.lyon8(prof, dm, out=out)
+    else:
+        import numpy as np
+
+        from pulsarfeatureextractor_amd.synth import bates_batch
+
+        # a 16384-candidate synthetic block (SURVEY.md §8(d) recipe), tiled to n rows in HBM
+        base = bates_batch(16384, lp=args.lp, lsb=args.lp, seed=20261018 + rank)
+        reps = (n + 16383) // 16384
+        bt = {}
+        for k, v in base.items():
+            t = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+            bt[k] = t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
+        out = torch.empty((n, 22), dtype=torch.float64, device=dev)
+        status = torch.empty((n,), dtype=torch.int32, device=dev)
+
+        def step():
+            eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out, status=status)
+    torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # kernel-duration events on the kernel's own stream
+    # step-duration events on the kernels' own stream
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     if dist_on:
@@ -150,7 +205,7 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
     if dist_on:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
     else:
@@ -158,12 +213,7 @@ def main():
 
     total_rows = n * world * args.steps
     value = total_rows / elapsed
-    bytes_per_launch = n * (args.lp + args.ld + 8 * 8)
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(f"lyon8_u8_{args.lp}x{args.ld}_n{n}_pmc.json")
-
-    result = {
-        "metric": "candidates/sec (8-feature path, 128-bin)",
+    common = {
         "value": value,
         "unit": "candidates/sec",
         "n_gpus": world,
@@ -173,29 +223,65 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8->int64/f64",
         "data": "synthetic (SURVEY.md §8(d) recipe, generated on device)",
-        "config": {
-            "workload": f"config 2: {n} synthetic candidates per GPU, {args.lp}-bin profile + "
-                        f"{args.ld}-bin DM, 8 Lyon moment features (pfe_lyon8_u8)",
-            "candidates_per_gpu": n,
-            "profile_bins": args.lp,
-            "dm_bins": args.ld,
-            "parallelism": f"candidate shards x{world}, no collective",
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "kernel": "pfe::lyon8_u8_fast3<128, 2>",
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "avg_kernel_ms": kern_ms,
-            "avg_kernel_ms_max_over_ranks": kern_ms_max,
-        },
     }
+    if args.path == "lyon8":
+        bytes_per_launch = n * (args.lp + args.ld + 8 * 8)
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(f"lyon8_u8_{args.lp}x{args.ld}_n{n}_pmc.json")
+        result = {
+            "metric": "candidates/sec (8-feature path, 128-bin)",
+            **common,
+            "dtype": "u8->int64/f64",
+            "config": {
+                "workload": f"config 2: {n} synthetic candidates per GPU, {args.lp}-bin profile + "
+                            f"{args.ld}-bin DM, 8 Lyon moment features (pfe_lyon8_u8)",
+                "candidates_per_gpu": n,
+                "profile_bins": args.lp,
+                "dm_bins": args.ld,
+                "parallelism": f"candidate shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "pfe::lyon8_u8_fast3<128, 2>",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "avg_kernel_ms": kern_ms,
+                "avg_kernel_ms_max_over_ranks": kern_ms_max,
+            },
+        }
+    else:
+        ops = load_ops_per_candidate()
+        achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
+        result = {
+            "metric": "candidates/sec (22-score path, 128-bin)",
+            **common,
+            "dtype": "f64",
+            "config": {
+                "workload": f"config 3 shape: {n} synthetic candidates per GPU, {args.lp}-bin "
+                            f"profile, 16x{args.lp} sub-bands, 128-point DM curve, 22 Bates "
+                            f"scores (pfe_bates22)",
+                "candidates_per_gpu": n,
+                "profile_bins": args.lp,
+                "parallelism": f"candidate shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "fp64-valu",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                "traffic": None,
+                "kernel": "pfe_bates22 (8 kernels, one step)",
+                "algorithmic_ops_per_candidate": ops,
+                "avg_step_ms": kern_ms,
+                "avg_step_ms_max_over_ranks": kern_ms_max,
+            },
+        }
     if args.gather and dist_on:
         # the optional reassembly step (RCCL all-gather of the n*world x 8 fp64 matrix over
         # xGMI), timed on its own, outside the headline step
@@ -212,7 +298,10 @@ def main():
         result["gather"] = {"ms": gms, "bytes_received_per_rank": int(full.numel() * 8 * (world - 1) / world),
                             "collective": "all_gather_into_tensor (RCCL)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
+        if args.path == "lyon8":
+            result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
+        else:
+            result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

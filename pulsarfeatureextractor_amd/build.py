@@ -48,8 +48,16 @@ def _needs(obj: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
-    os.makedirs(BUILDDIR, exist_ok=True)
+def build(verbose: bool = False, force: bool = False, variant: str = "",
+          defines: tuple[str, ...] = ()) -> str:
+    """Compile every source and link lib/libpfe.so.  A non-empty ``variant`` builds an
+    instrumented copy (lib/libpfe_<variant>.so, objects under lib/obj_<variant>/) with the
+    extra -D ``defines`` (e.g. the LM phase-cycle profiler, -DPFE_LM_PROFILE); the product
+    library is never built with them."""
+    builddir = BUILDDIR + (f"_{variant}" if variant else "")
+    lib = os.path.join(LIBDIR, f"libpfe_{variant}.so") if variant else LIB
+    extra = [f"-D{d}" for d in defines]
+    os.makedirs(builddir, exist_ok=True)
     cc = hipcc()
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "pfe.h"))
@@ -57,10 +65,10 @@ def build(verbose: bool = False, force: bool = False) -> str:
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILDDIR, src.replace(".hip", ".o"))
+        o = os.path.join(builddir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _needs(o, [s] + headers):
-            jobs.append([cc, *COMMON, "-c", s, "-o", o])
+            jobs.append([cc, *COMMON, *extra, "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -72,12 +80,16 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    if force or jobs or not os.path.exists(LIB):
-        tmp = LIB + ".tmp"
+    if force or jobs or not os.path.exists(lib):
+        tmp = lib + ".tmp"
         run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
-        os.replace(tmp, LIB)
-    return LIB
+        os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    if "--lm-profile" in sys.argv:
+        print(build(verbose=True, force="--force" in sys.argv, variant="lmprof",
+                    defines=("PFE_LM_PROFILE",)))
+    else:
+        print(build(verbose=True, force="--force" in sys.argv))

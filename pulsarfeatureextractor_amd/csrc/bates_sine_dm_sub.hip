@@ -499,3 +499,5 @@ hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
 }
 
 }  // namespace pfe
+
+PFE_LM_PROFILE_EXPORT(sine_dm_sub)

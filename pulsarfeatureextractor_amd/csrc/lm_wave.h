@@ -29,6 +29,43 @@ constexpr double LM_FACTOR = 100.0;
 constexpr double EPSMCH = 2.220446049250313e-16;
 constexpr double DWARF = 2.2250738585072014e-308;
 
+// ---- optional phase-cycle profiler (instrumented builds only: -DPFE_LM_PROFILE) ----------
+// Per translation unit, per parameter count N (slot 0..3 for N = 2, 3, 4, 8): counters
+//   0 lmdif calls, 1 outer iterations, 2 lmpar calls, 3 qrsolv calls, 4 function evaluations,
+//   5 fdjac2 cycles, 6 qrfac cycles, 7 Q^T f / R / gnorm cycles, 8 lmpar cycles,
+//   9 trial evaluation cycles, 10 total lmdif cycles
+#ifdef PFE_LM_PROFILE
+static __device__ unsigned long long pfe_lm_prof[4][16];
+__device__ __forceinline__ long long lm_clock() { return clock64(); }
+template <int N>
+__device__ __forceinline__ void lm_prof_add(int k, long long v) {
+  constexpr int slot = N == 2 ? 0 : N == 3 ? 1 : N == 4 ? 2 : 3;
+  if (lane_id() == 0) atomicAdd(&pfe_lm_prof[slot][k], (unsigned long long)v);
+}
+#define PFE_LM_PROFILE_EXPORT(tag)                                                      \
+  extern "C" int pfe_lmprof_##tag(unsigned long long* out, int reset) {                 \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pfe::pfe_lm_prof), sizeof(pfe::pfe_lm_prof)) != \
+        hipSuccess)                                                                     \
+      return -1;                                                                        \
+    if (reset) {                                                                        \
+      static unsigned long long z[4][16];                                               \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(pfe::pfe_lm_prof), z, sizeof(z)) != hipSuccess)  \
+        return -1;                                                                      \
+    }                                                                                   \
+    return 0;                                                                           \
+  }
+#define LM_T0(v) const long long v = lm_clock()
+#define LM_ADD(k, v) lm_prof_add<N>((k), (v))
+#else
+#define PFE_LM_PROFILE_EXPORT(tag)
+#define LM_T0(v) \
+  do {           \
+  } while (0)
+#define LM_ADD(k, v) \
+  do {               \
+  } while (0)
+#endif
+
 // MINPACK enorm of a replicated n-vector (sequential, with the dwarf/giant scaling)
 template <int N>
 __device__ __forceinline__ double enorm_u(const double (&x)[N]) {
@@ -325,6 +362,7 @@ __device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
 #pragma unroll
     for (int j = 0; j < N; ++j) wa1[j] = sp * diag[j];
     qrsolv<N>(r, ipvt, wa1, qtb, x, sdiag);
+    LM_ADD(3, 1);
 #pragma unroll
     for (int j = 0; j < N; ++j) wa2[j] = diag[j] * x[j];
     dxnorm = enorm_u(wa2);
@@ -368,6 +406,7 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
   double r[N][N];
   int ipvt[N];
   int info = 0;
+  LM_T0(t_start);
   fcn(x, fvec);
   int nfev = 1;
   double fnorm = enorm_w(fvec);
@@ -375,6 +414,8 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
   int iter = 1;
   const int lane = lane_id();
   for (;;) {
+    LM_ADD(1, 1);
+    LM_T0(t_fd);
     // forward-difference Jacobian (fdjac2)
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -388,7 +429,11 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
       for (int k = 0; k < MPL; ++k) fjac[k][j] = (wa4[k] - fvec[k]) / h;
     }
     nfev += N;
+    LM_T0(t_qr);
+    LM_ADD(5, t_qr - t_fd);
     qrfac<N, MPL>(fjac, ipvt, wa1, wa2);
+    LM_T0(t_qt);
+    LM_ADD(6, t_qt - t_qr);
     if (iter == 1) {
 #pragma unroll
       for (int j = 0; j < N; ++j) {
@@ -440,6 +485,8 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
         }
       }
     }
+    LM_T0(t_gn);
+    LM_ADD(7, t_gn - t_qt);
     if (gnorm <= LM_GTOL) info = 4;
     if (info != 0) break;
 #pragma unroll
@@ -447,7 +494,11 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
     // inner loop
     double ratio;
     do {
+      LM_T0(t_lp);
       lmpar<N>(r, ipvt, diag, qtf, delta, par, wa1, wa2);
+      LM_T0(t_tr);
+      LM_ADD(8, t_tr - t_lp);
+      LM_ADD(2, 1);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         wa1[j] = -wa1[j];
@@ -459,6 +510,7 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
       fcn(wa2, wa4);
       ++nfev;
       const double fnorm1 = enorm_w(wa4);
+      LM_ADD(9, lm_clock() - t_tr);
       double actred = -1.0;
       if (0.1 * fnorm1 < fnorm) {
         const double q = fnorm1 / fnorm;
@@ -513,6 +565,9 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
     } while (ratio < 1e-4);
     if (info != 0) break;
   }
+  LM_ADD(0, 1);
+  LM_ADD(4, nfev);
+  LM_ADD(10, lm_clock() - t_start);
   return {info, nfev};
 }
 

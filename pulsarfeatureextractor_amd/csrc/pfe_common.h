@@ -66,14 +66,26 @@ __device__ __forceinline__ long long wave_sum_i64(long long v) {
   return (long long)u;
 }
 
+// Combine the four 16-lane row sums of a wave (each row holds its sum in every lane) as
+// (row0 + row1) + (row2 + row3) -- the same tree as xor-16 then xor-32 butterflies -- through
+// lane reads, so the result is provably wave-uniform (scalar branches downstream) and no
+// LDS-routed permutes are on the critical path.  Requires every lane active.
+__device__ __forceinline__ double lane_f64(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)b >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ double row_total_f64(double v) {
+  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+
 __device__ __forceinline__ double wave_sum_f64(double v) {
   v += dpp_f64<DPP_QUAD_XOR1>(v);
   v += dpp_f64<DPP_QUAD_XOR2>(v);
   v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
   v += dpp_f64<DPP_ROW_MIRROR>(v);
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+  return row_total_f64(v);
 }
 
 }  // namespace pfe

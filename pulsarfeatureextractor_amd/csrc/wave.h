@@ -12,12 +12,7 @@ namespace pfe {
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // value of v held by lane `src` (src must be wave-uniform)
-__device__ __forceinline__ double bcast(double v, int src) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, src);
-  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)b >> 32), src);
-  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
-}
+__device__ __forceinline__ double bcast(double v, int src) { return lane_f64(v, src); }
 __device__ __forceinline__ int bcast_i(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 
 // make a value that is uniform in fact also uniform for the compiler (SGPR)
@@ -38,9 +33,7 @@ __device__ __forceinline__ void wsum_arr(double (&v)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) v[k] += dpp_f64<DPP_ROW_MIRROR>(v[k]);
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], 16);
-#pragma unroll
-  for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], 32);
+  for (int k = 0; k < K; ++k) v[k] = row_total_f64(v[k]);
 }
 
 __device__ __forceinline__ int wsum_i(int v) {

@@ -17,9 +17,12 @@ def main():
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lp", type=int, default=128)
+    ap.add_argument("--lib", default=None, help="alternative libpfe build (A/B runs)")
+    ap.add_argument("--save", default=None, help="write scores/status to this .npz")
     args = ap.parse_args()
     import torch
 
+    from pulsarfeatureextractor_amd import _native
     from pulsarfeatureextractor_amd._native import Engine
     from pulsarfeatureextractor_amd.synth import bates_batch
 
@@ -27,6 +30,8 @@ def main():
     reps = (args.n + 4095) // 4096
     t = {k: torch.from_numpy(np.ascontiguousarray(np.concatenate([v] * reps)[: args.n])).cuda()
          for k, v in base.items()}
+    if args.lib:
+        _native._lib = _native.load_library(os.path.abspath(args.lib))
     eng = Engine(0)
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
@@ -43,6 +48,8 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     best = min(times)
+    if args.save:
+        np.savez_compressed(args.save, out=out.cpu().numpy(), status=st.cpu().numpy())
     print(json.dumps({"n": args.n, "lp": args.lp, "seconds": times,
                       "candidates_per_sec": args.n / best,
                       "failures": int(((st & 0xFF) != 0).sum().item())}))
