@@ -15,8 +15,27 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st);
 hipError_t launch_subband(const BatesArgs& a, hipStream_t st);
 
+// persistent waves of the batched kernels: enough to fill every CU (8 waves each), never
+// more than there are batches
+static int persistent_waves(int64_t n) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+  }
+  const int64_t batches = (n + BLM_FPW - 1) / BLM_FPW;
+  const int64_t w = (int64_t)cus * 8;
+  return (int)(batches < w ? (batches > 0 ? batches : 1) : w);
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// workspace layout: [GaussWS x n][counters][per-wave scratch]
 size_t bates22_workspace_bytes(const pfe_bates_in* in) {
-  return (size_t)in->n * sizeof(GaussWS) + 256;
+  return 256 + align256((size_t)in->n * sizeof(GaussWS)) +
+         align256(BATES_NCOUNTERS * sizeof(unsigned)) +
+         (size_t)persistent_waves(in->n) * gdg_wave_scratch_doubles(in->lp) * sizeof(double);
 }
 
 __global__ void k_clear_internal(uint32_t* status, int64_t n) {
@@ -39,13 +58,21 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   a.n = in->n;
   a.out = out;
   a.status = status;
-  a.ws = (GaussWS*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
+  char* wb = (char*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
+  a.ws = (GaussWS*)wb;
+  wb += align256((size_t)in->n * sizeof(GaussWS));
+  a.counters = (unsigned*)wb;
+  wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
+  a.wscr = (double*)wb;
+  a.pwaves = persistent_waves(in->n);
   // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code
   a.c_lp = std::pow((double)in->lp, -0.3333333);
   a.c_lp1 = std::pow((double)(in->lp - 1), -0.3333333);
   hipError_t e = hipMemsetAsync(status, 0, (size_t)in->n * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(out, 0, (size_t)in->n * 22 * sizeof(double), st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(a.counters, 0, BATES_NCOUNTERS * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
   if ((e = launch_sine(a, st)) != hipSuccess) return e;
   if ((e = launch_gauss(a, st)) != hipSuccess) return e;

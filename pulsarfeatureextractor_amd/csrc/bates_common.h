@@ -43,7 +43,23 @@ struct BatesArgs {
   GaussWS* ws;       // n
   double c_lp;       // pow(lp, -0.3333333)     (ProfileOperationsInterface.py:151)
   double c_lp1;      // pow(lp-1, -0.3333333)
+  unsigned* counters;  // BATES_NCOUNTERS work-queue counters, zeroed before the chain
+  double* wscr;        // per-wave scratch of the persistent batched kernels
+  int pwaves;          // number of persistent waves wscr is sized for
 };
+
+constexpr int BATES_NCOUNTERS = 16;
+constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
+constexpr int BLM_FPW = 32;  // fits per wave in the batched kernels
+
+// rows per lane (MPL) the kernels use for a profile of lp bins
+__host__ __device__ constexpr int profile_mpl(int lp) {
+  return lp <= 64 ? 1 : lp <= 128 ? 2 : lp <= 256 ? 4 : 16;
+}
+// per-wave scratch of k_gdgb: x and y of FPW fits, 64*MPL rows each
+__host__ __device__ constexpr size_t gdg_wave_scratch_doubles(int lp) {
+  return (size_t)BLM_FPW * 64 * profile_mpl(lp) * 2;
+}
 
 static inline dim3 grid_for_candidates(int64_t n) {
   return dim3((unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));

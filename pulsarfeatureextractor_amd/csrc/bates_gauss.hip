@@ -14,6 +14,7 @@
 //   k_gdg    : peak peeling, 8 single-Gaussian passes with subtraction, the 8-parameter
 //              fit and the combination rule -> s10, s11
 #include "bates_common.h"
+#include "lm_batch.h"
 
 namespace pfe {
 
@@ -448,10 +449,22 @@ __global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
 // ---------------------------------------------------------------------------------------
 // s10, s11: fitDoubleGaussianT2 -> fitDoubleGaussian -> fitDoubleGaussianWithBackground
 // ---------------------------------------------------------------------------------------
+// Residual functors used by the batched solver also provide eval (full evaluation that
+// keeps the exp terms) and eval_col (evaluation at a point that differs from the cached one
+// only in parameter j): forward-difference columns of amplitude/background parameters then
+// reuse the exp terms.  Same operations on the same operands, so bit-identical residuals.
 template <int MPL>
 struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
+  static constexpr bool kCols = true;
+  struct Cache {
+    double e[MPL];
+  };
   double x[MPL], y[MPL];
   bool ok[MPL];
+  __device__ __forceinline__ double term(const double (&p)[4], int k) const {
+    const double t = (x[k] - p[1]) / p[0];
+    return exp(-(t * t) / 2.0);
+  }
   __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
@@ -463,6 +476,21 @@ struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
       }
     }
   }
+  __device__ __forceinline__ void eval(const double (&p)[4], double (&f)[MPL], Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      c.e[k] = ok[k] ? term(p, k) : 0.0;
+      f[k] = ok[k] ? y[k] - (fabs(p[2]) * c.e[k] + fabs(p[3])) : 0.0;
+    }
+  }
+  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double (&f)[MPL],
+                                           const Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      const double e = (j < 2) ? (ok[k] ? term(p, k) : 0.0) : c.e[k];
+      f[k] = ok[k] ? y[k] - (fabs(p[2]) * e + fabs(p[3])) : 0.0;
+    }
+  }
 };
 __device__ __forceinline__ double g_absbg(double x, const double (&p)[4]) {
   const double t = (x - p[1]) / p[0];
@@ -471,17 +499,46 @@ __device__ __forceinline__ double g_absbg(double x, const double (&p)[4]) {
 
 template <int MPL>
 struct DoubleGaussFn {  // :1459-1460
+  static constexpr bool kCols = true;
+  struct Cache {
+    double e1[MPL], e2[MPL];
+  };
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ __forceinline__ double model(const double (&p)[8], int k) const {
+  __device__ __forceinline__ double term1(const double (&p)[8], int k) const {
     const double t1 = (x[k] - p[1]) / fabs(p[0]);
+    return exp(-(t1 * t1) / 2.0);
+  }
+  __device__ __forceinline__ double term2(const double (&p)[8], int k) const {
     const double t2 = (x[k] - p[5]) / fabs(p[4]);
-    return (fabs(p[2]) * exp(-(t1 * t1) / 2.0)) + (fabs(p[6]) * exp(-(t2 * t2) / 2.0)) +
-           (fabs(p[3]) + fabs(p[7])) / 2.0;
+    return exp(-(t2 * t2) / 2.0);
+  }
+  __device__ __forceinline__ double combine(const double (&p)[8], double e1, double e2) const {
+    return (fabs(p[2]) * e1) + (fabs(p[6]) * e2) + (fabs(p[3]) + fabs(p[7])) / 2.0;
+  }
+  __device__ __forceinline__ double model(const double (&p)[8], int k) const {
+    return combine(p, term1(p, k), term2(p, k));
   }
   __device__ __forceinline__ void operator()(const double (&p)[8], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+  __device__ __forceinline__ void eval(const double (&p)[8], double (&f)[MPL], Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      c.e1[k] = ok[k] ? term1(p, k) : 0.0;
+      c.e2[k] = ok[k] ? term2(p, k) : 0.0;
+      f[k] = ok[k] ? y[k] - combine(p, c.e1[k], c.e2[k]) : 0.0;
+    }
+  }
+  __device__ __forceinline__ void eval_col(const double (&p)[8], int j, double (&f)[MPL],
+                                           const Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      const double e1 = (j == 0 || j == 1) ? (ok[k] ? term1(p, k) : 0.0) : c.e1[k];
+      const double e2 = (j == 4 || j == 5) ? (ok[k] ? term2(p, k) : 0.0) : c.e2[k];
+      f[k] = ok[k] ? y[k] - combine(p, e1, e2) : 0.0;
+    }
   }
 };
 
@@ -521,24 +578,21 @@ struct KeptSet {
   }
 };
 
+// fitDoubleGaussianT2 (:1162-1170) and the peak removal of fitDoubleGaussian (:1305-1354)
+// for candidate c: y/ok = the rotated integer profile (also in ys, LDS); the kept points'
+// positions are compacted into cx[0..m1) (LDS).  Returns m1, or -1 on the reference's
+// IndexError (then s10 = s11 = 1e6 are written and the status bit is set).
 template <int P>
-__global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
-  __shared__ int ys_all[BLOCK / 64][64 * P];
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+__device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, int* ys, double* cx, int (&y)[P],
+                        bool (&ok)[P]) {
   const int lane = lane_id();
   const int L = a.lp;
   const int cut = L / 2;
-  int* ys = ys_all[threadIdx.x >> 6];
-  // rotated integer profile (fitDoubleGaussianT2 :1162-1170)
-  int y[P];
-  bool ok[P];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int i = lane + 64 * k;
     ok[k] = i < L;
-    y[k] = ok[k] ? (int)a.prof[c * L + (i + cut) % L] : -1;
+    y[k] = ok[k] ? (int)a.prof[c * L + (ok[k] ? (i + cut) % L : 0)] : -1;
     if (ok[k]) ys[i] = y[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -611,13 +665,9 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
       a.out[c * 22 + 10] = 1000000.0;
       a.status[c] |= PFE_ST_DGF_INDEXERROR;
     }
-    return;
+    return -1;
   }
-  // ---- pass 1 on the compacted kept points, passes 2..8 on all L points
-  GaussAbsBgFn<P> fn;
-  // compaction through LDS: write (x, y) of kept points to rows 0..len-1
-  __shared__ double cx_all[BLOCK / 64][64 * P];
-  double* cx = cx_all[threadIdx.x >> 6];
+  // compaction through LDS: x of the kept points to rows 0..len-1
   {
     int rank_base = 0;
 #pragma unroll
@@ -633,7 +683,86 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  const int m1 = ks.len;
+  return ks.len;
+}
+
+// start point of a peel pass from the current data rows [0, nlen) (:1361-1367)
+template <int P>
+__device__ __forceinline__ void peel_start(const GaussAbsBgFn<P>& fn, int nlen, double (&p)[4]) {
+  const int lane = lane_id();
+  double bvd = -INFINITY;
+  int bid = 1 << 30;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int r = lane + 64 * k;
+    if (r < nlen) {
+      s += fn.y[k];
+      if (bid == (1 << 30) || fn.y[k] > bvd) {
+        bvd = fn.y[k];
+        bid = r;
+      }
+    }
+  }
+  const ArgMax am = wargmax(bvd, bid);
+  const double mean = wsum(s) / (double)nlen;
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (lane + 64 * k < nlen) q += (fn.y[k] - mean) * (fn.y[k] - mean);
+  double xe = 0.0;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (am.i >> 6 == k) xe = bcast(fn.x[k], am.i & 63);
+  p[0] = sqrt(wsum(q) / (double)nlen);
+  p[1] = xe;
+  p[2] = am.v;
+  p[3] = mean;
+}
+
+// subtraction of a peel pass's fit from the rotated profile y (:1389-1399; the window is
+// centred on p[2], the amplitude): new data rows into fn
+template <int P>
+__device__ __forceinline__ void peel_subtract(const int (&y)[P], const bool (&ok)[P],
+                                              const double (&p)[4], GaussAbsBgFn<P>& fn) {
+  const int lane = lane_id();
+  const double nfwhm = fabs(FWHM_C * p[0]);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    const double xi = (double)i;
+    const double yi = (double)y[k];
+    double ny = yi;
+    if (ok[k]) {
+      const double ev = g_absbg(xi, p);
+      if (ev <= yi)
+        ny = yi - ev + p[3];
+      else if ((ev > yi) && (xi > (p[2] - (1.5 * nfwhm) / 2.0)) && (xi < (p[2] + (1.5 * nfwhm) / 2.0)))
+        ny = p[3];
+    }
+    fn.x[k] = xi;
+    fn.y[k] = ok[k] ? ny : 0.0;
+    fn.ok[k] = ok[k];
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
+  __shared__ int ys_all[BLOCK / 64][64 * P];
+  __shared__ double cx_all[BLOCK / 64][64 * P];
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  const int lane = lane_id();
+  const int L = a.lp;
+  int* ys = ys_all[threadIdx.x >> 6];
+  double* cx = cx_all[threadIdx.x >> 6];
+  int y[P];
+  bool ok[P];
+  const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
+  if (m1 < 0) return;
+  GaussAbsBgFn<P> fn;
+  // ---- pass 1 on the compacted kept points, passes 2..8 on all L points
   double cy[P];
   bool cok[P];
 #pragma unroll
@@ -648,55 +777,9 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
   double p[4], p1[4], p2[4];
   int nlen = m1;
   for (int pass = 1; pass <= 8; ++pass) {
-    // initial parameters from the current data (before padding) (:1361-1367)
-    double bvd = -INFINITY;
-    int bid = 1 << 30;
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int r = lane + 64 * k;
-      if (r < nlen) {
-        s += fn.y[k];
-        if (bid == (1 << 30) || fn.y[k] > bvd) {
-          bvd = fn.y[k];
-          bid = r;
-        }
-      }
-    }
-    const ArgMax am = wargmax(bvd, bid);
-    const double mean = wsum(s) / (double)nlen;
-    double q = 0.0;
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-      if (lane + 64 * k < nlen) q += (fn.y[k] - mean) * (fn.y[k] - mean);
-    double xe = 0.0;
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-      if (am.i >> 6 == k) xe = bcast(fn.x[k], am.i & 63);
-    p[0] = sqrt(wsum(q) / (double)nlen);
-    p[1] = xe;
-    p[2] = am.v;
-    p[3] = mean;
+    peel_start<P>(fn, nlen, p);
     lmdif<4, P>(fn, p, 200 * 5);
-    const double nfwhm = fabs(FWHM_C * p[0]);
-    // subtraction (:1389-1399; window centred on p[2], the amplitude)
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int i = lane + 64 * k;
-      const double xi = (double)i;
-      const double yi = (double)y[k];
-      double ny = yi;
-      if (ok[k]) {
-        const double ev = g_absbg(xi, p);
-        if (ev <= yi)
-          ny = yi - ev + p[3];
-        else if ((ev > yi) && (xi > (p[2] - (1.5 * nfwhm) / 2.0)) && (xi < (p[2] + (1.5 * nfwhm) / 2.0)))
-          ny = p[3];
-      }
-      fn.x[k] = xi;
-      fn.y[k] = ok[k] ? ny : 0.0;
-      fn.ok[k] = ok[k];
-    }
+    peel_subtract<P>(y, ok, p, fn);
     nlen = L;
     if (pass == 7) {
 #pragma unroll
@@ -716,35 +799,153 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
   }
 }
 
-// final 8-parameter fit (:1411, :1432-1483), the combination rule (:1413-1428) and the
-// s10/s11 selection of getGaussianFittings (:747-768)
+// Batched form of k_gdg: persistent waves take batches of BLM_FPW candidates from a queue;
+// the 8 peel passes run as 8 batched lmdif calls (lm_batch.h) over the batch's fits.  Each
+// fit's data rows (x, y) live in the wave's scratch between m-phase visits.
 template <int P>
-__global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) return;
+struct PeelLoader {
+  const double* xs;  // [FPW][64P]
+  const double* ys;
+  const int* mpad;   // LDS [FPW]: rows [0, mpad) take part (zero padding included)
+  __device__ __forceinline__ GaussAbsBgFn<P> operator()(int f) const {
+    GaussAbsBgFn<P> fn;
+    const int lane = lane_id();
+    const int mp = mpad[f];
+    const double* X = xs + (size_t)f * 64 * P;
+    const double* Y = ys + (size_t)f * 64 * P;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int r = lane + 64 * k;
+      fn.x[k] = X[r];
+      fn.y[k] = Y[r];
+      fn.ok[k] = r < mp;
+    }
+    return fn;
+  }
+};
+
+__device__ __forceinline__ void scratch_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+template <int P>
+__device__ __forceinline__ void store_rows(double* X, double* Y, const GaussAbsBgFn<P>& fn) {
   const int lane = lane_id();
-  const int L = a.lp;
-  const int cut = L / 2;
-  const GaussWS w = a.ws[c];
-  bool ok[P];
-  DoubleGaussFn<P> dg;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    const int i = lane + 64 * k;
-    ok[k] = i < L;
-    dg.x[k] = (double)i;
-    dg.y[k] = ok[k] ? (double)a.prof[c * L + (i + cut) % L] : 0.0;
-    dg.ok[k] = ok[k];
+    X[lane + 64 * k] = fn.x[k];
+    Y[lane + 64 * k] = fn.y[k];
   }
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
+  constexpr int FPW = BLM_FPW;
+  __shared__ BlmState<4, FPW> S;
+  __shared__ int ys[64 * P];
+  __shared__ double cx[64 * P];
+  __shared__ int mpad[FPW];
+  const int lane = lane_id();
+  const int L = a.lp;
+  double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(L);
+  double* yv = xs + (size_t)FPW * 64 * P;
+  const PeelLoader<P> load{xs, yv, mpad};
+  const int64_t nb = (a.n + FPW - 1) / FPW;
+  for (;;) {
+    int b = 0;
+    if (lane == 0) b = (int)atomicAdd(a.counters + CTR_GDG, 1u);
+    b = __builtin_amdgcn_readfirstlane(b);
+    if (b >= nb) break;
+    const int64_t base = (int64_t)b * FPW;
+    // candidates of this batch that reach the double-Gaussian fit
+    const bool live = lane < FPW && base + lane < a.n &&
+                      !(a.status[base + (lane < FPW ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
+    uint64_t fits = __ballot(live);
+    // prologue: peak removal, pass-1 rows and start points
+    for (uint64_t m = fits; m; m &= m - 1) {
+      const int f = __builtin_ctzll(m);
+      const int64_t c = base + f;
+      int y[P];
+      bool ok[P];
+      const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
+      if (m1 < 0) {
+        fits &= ~(1ull << f);
+        continue;
+      }
+      GaussAbsBgFn<P> fn;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int r = lane + 64 * k;
+        const bool cok = r < m1;
+        fn.x[k] = cok ? cx[r] : 0.0;
+        fn.y[k] = cok ? (double)ys[(int)fn.x[k]] : 0.0;
+        fn.ok[k] = r < (m1 < 4 ? 4 : m1);  // zero padding to 4 points (:1373-1377)
+      }
+      store_rows<P>(xs + (size_t)f * 64 * P, yv + (size_t)f * 64 * P, fn);
+      double p[4];
+      peel_start<P>(fn, m1, p);
+      if (lane == 0) {
+        mpad[f] = m1 < 4 ? 4 : m1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S.x[j][f] = p[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (fits == 0) continue;
+    scratch_sync();
+    for (int pass = 1; pass <= 8; ++pass) {
+      blm_run<4, P, FPW>(load, S, fits, 200 * 5);
+      for (uint64_t m = fits; m; m &= m - 1) {
+        const int f = __builtin_ctzll(m);
+        const int64_t c = base + f;
+        double p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = S.x[j][f];
+        if (pass >= 7 && lane == 0) {
+          GaussWS* wp = a.ws + c;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wp->dg[(pass == 8 ? 0 : 4) + j] = p[j];
+        }
+        if (pass == 8) continue;
+        int y[P];
+        bool ok[P];
+        const int cut = L / 2;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const int i = lane + 64 * k;
+          ok[k] = i < L;
+          y[k] = ok[k] ? (int)a.prof[c * L + (ok[k] ? (i + cut) % L : 0)] : -1;
+        }
+        GaussAbsBgFn<P> fn;
+        peel_subtract<P>(y, ok, p, fn);
+        store_rows<P>(xs + (size_t)f * 64 * P, yv + (size_t)f * 64 * P, fn);
+        double q[4];
+        peel_start<P>(fn, L, q);
+        if (lane == 0) {
+          mpad[f] = L;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) S.x[j][f] = q[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      scratch_sync();
+    }
+  }
+}
+
+// the combination rule (:1413-1428) and the s10/s11 selection (:747-768) after the final fit
+template <int P>
+__device__ __forceinline__ void gdg8_finish(const BatesArgs& a, int64_t c, const DoubleGaussFn<P>& dg,
+                                            const bool (&ok)[P], const double (&q8)[8],
+                                            const GaussWS& w) {
+  const int lane = lane_id();
+  const int L = a.lp;
   double p1[4], p2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     p1[j] = w.dg[j];
     p2[j] = w.dg[4 + j];
   }
-  double q8[8] = {p1[0], p1[1], p1[2], p1[3], p2[0], p2[1], p2[2], p2[3]};
-  lmdif<8, P>(dg, q8, 200 * 9);
   const double f_fwhm1 = fabs(FWHM_C * q8[0]), f_fwhm2 = fabs(FWHM_C * q8[4]);
   double fchi = 0.0, cchi = 0.0;
   double ffit[P], cfit[P];
@@ -789,18 +990,120 @@ __global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
   }
 }
 
+// final 8-parameter fit (:1411, :1432-1483), the combination rule (:1413-1428) and the
+// s10/s11 selection of getGaussianFittings (:747-768)
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) return;
+  const int lane = lane_id();
+  const int L = a.lp;
+  const int cut = L / 2;
+  const GaussWS w = a.ws[c];
+  bool ok[P];
+  DoubleGaussFn<P> dg;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    ok[k] = i < L;
+    dg.x[k] = (double)i;
+    dg.y[k] = ok[k] ? (double)a.prof[c * L + (i + cut) % L] : 0.0;
+    dg.ok[k] = ok[k];
+  }
+  double p1[4], p2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p1[j] = w.dg[j];
+    p2[j] = w.dg[4 + j];
+  }
+  double q8[8] = {p1[0], p1[1], p1[2], p1[3], p2[0], p2[1], p2[2], p2[3]};
+  lmdif<8, P>(dg, q8, 200 * 9);
+  gdg8_finish<P>(a, c, dg, ok, q8, w);
+}
+
+// Batched form of k_gdg8: one wave owns FPW candidates and runs their 8-parameter fits
+// through the batched lmdif (lm_batch.h); bit-identical to k_gdg8.
+template <int P>
+struct Gdg8Loader {
+  const uint8_t* prof;
+  int64_t base;
+  int L, cut;
+  __device__ __forceinline__ DoubleGaussFn<P> operator()(int f) const {
+    DoubleGaussFn<P> dg;
+    const int lane = lane_id();
+    const uint8_t* row = prof + (base + f) * L;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int i = lane + 64 * k;
+      const bool ok = i < L;
+      dg.x[k] = (double)i;
+      dg.y[k] = ok ? (double)row[ok ? (i + cut) % L : 0] : 0.0;
+      dg.ok[k] = ok;
+    }
+    return dg;
+  }
+};
+
+template <int P, int FPW>
+__global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
+  __shared__ BlmState<8, FPW> S;
+  const int64_t base = (int64_t)blockIdx.x * FPW;
+  const int lane = lane_id();
+  bool part = false;
+  if (lane < FPW) {
+    const int64_t c = base + lane;
+    if (c < a.n && !(a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR))) {
+      part = true;
+      const GaussWS* w = a.ws + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) S.x[j][lane] = w->dg[j];
+    }
+  }
+  const uint64_t fits = __ballot(part);
+  if (fits == 0) return;
+  const int L = a.lp;
+  const Gdg8Loader<P> load{a.prof, base, L, L / 2};
+  blm_run<8, P, FPW>(load, S, fits, 200 * 9);
+  for (uint64_t m = fits; m; m &= m - 1) {
+    const int f = __builtin_ctzll(m);
+    const int64_t c = base + f;
+    const DoubleGaussFn<P> dg = load(f);
+    bool ok[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) ok[k] = dg.ok[k];
+    double q8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q8[j] = S.x[j][f];
+    const GaussWS w = a.ws[c];
+    gdg8_finish<P>(a, c, dg, ok, q8, w);
+  }
+}
+
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }
 
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const int L = a.lp;
+  // batched lmdif (lm_batch.h) unless PFE_BLM=0 selects the wave-per-fit kernels (A/B runs)
+  static const bool use_blm = [] {
+    const char* e = getenv("PFE_BLM");
+    return !(e && e[0] == '0');
+  }();
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
     hipLaunchKernelGGL((k_ghist<P, 4, false>), gw(a.n), dim3(BLOCK), 0, st, a);         \
     hipLaunchKernelGGL((k_ghist<P, 16, true>), gw(a.n), dim3(BLOCK), 0, st, a);         \
     hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
-    hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
-    hipLaunchKernelGGL((k_gdg8<P>), gw(a.n), dim3(BLOCK), 0, st, a);                    \
+    if (use_blm)                                                                        \
+      hipLaunchKernelGGL((k_gdgb<P>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);    \
+    else                                                                                \
+      hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
+    if (use_blm)                                                                        \
+      hipLaunchKernelGGL((k_gdg8b<P, BLM_FPW>), dim3((unsigned)((a.n + BLM_FPW - 1) / BLM_FPW)), \
+                         dim3(64), 0, st, a);                                           \
+    else                                                                                \
+      hipLaunchKernelGGL((k_gdg8<P>), gw(a.n), dim3(BLOCK), 0, st, a);                  \
   } while (0)
   if (L <= 64)
     PFE_GAUSS_LAUNCH(1);

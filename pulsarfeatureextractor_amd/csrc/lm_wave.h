@@ -193,7 +193,7 @@ __device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], doubl
           }
           d[c] = q;
         }
-        wsum_arr(d);
+        wsum_from(d, j + 1);
         const double ajj = bcast(a[0][j], j);
 #pragma unroll
         for (int c = j + 1; c < N; ++c) {

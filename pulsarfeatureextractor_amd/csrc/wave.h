@@ -36,6 +36,26 @@ __device__ __forceinline__ void wsum_arr(double (&v)[K]) {
   for (int k = 0; k < K; ++k) v[k] = row_total_f64(v[k]);
 }
 
+// wsum_arr restricted to v[lo..K) (lo folds to a constant inside unrolled loops)
+template <int K>
+__device__ __forceinline__ void wsum_from(double (&v)[K], int lo) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_QUAD_XOR1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_QUAD_XOR2>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_ROW_HALF_MIRROR>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_ROW_MIRROR>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] = row_total_f64(v[k]);
+}
+
 __device__ __forceinline__ int wsum_i(int v) {
   v += __shfl_xor(v, 1);
   v += __shfl_xor(v, 2);
