@@ -38,6 +38,17 @@ EXPORTED_SYMBOLS = (
     "pfe_lyon8_f64",
     "pfe_bates22",
 )
+# every symbol include/pfe_io.h declares
+EXPORTED_IO_SYMBOLS = (
+    "pfe_phcx_parse",
+    "pfe_phcx_count",
+    "pfe_phcx_info_get",
+    "pfe_phcx_fetch",
+    "pfe_phcx_pack",
+    "pfe_phcx_free",
+)
+PFE_PHCX_PROFILE, PFE_PHCX_LYON_DM, PFE_PHCX_SUBBANDS, PFE_PHCX_DM_CURVE, PFE_PHCX_FIT_BLOCK = range(5)
+PFE_IO_STATUS = {0: "ok", 1: "open", 2: "gzip", 3: "xml", 4: "value", 5: "range", 6: "shape"}
 
 
 class PfeError(RuntimeError):
@@ -55,6 +66,22 @@ class BatesIn(C.Structure):
         ("ndm", C.c_int32),
         ("scal", C.c_void_p),
         ("n", C.c_int64),
+    ]
+
+
+class PhcxInfo(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("superb", C.c_int32),
+        ("section", C.c_int32),
+        ("lp", C.c_int32),
+        ("nsub", C.c_int32),
+        ("lsb", C.c_int32),
+        ("ndm", C.c_int32),
+        ("reserved", C.c_int32),
+        ("ld", C.c_int64),
+        ("lfit", C.c_int64),
+        ("scal", C.c_double * 8),
     ]
 
 
@@ -119,6 +146,19 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_lyon8_f64.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
         lib.pfe_bates22.restype = C.c_int
         lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
+        pp = C.POINTER(C.c_char_p)
+        lib.pfe_phcx_parse.restype = C.c_int
+        lib.pfe_phcx_parse.argtypes = [pp, i64, i32, i32, C.POINTER(vp)]
+        lib.pfe_phcx_count.restype = i64
+        lib.pfe_phcx_count.argtypes = [vp]
+        lib.pfe_phcx_info_get.restype = C.c_int
+        lib.pfe_phcx_info_get.argtypes = [vp, i64, C.POINTER(PhcxInfo)]
+        lib.pfe_phcx_fetch.restype = C.c_int
+        lib.pfe_phcx_fetch.argtypes = [vp, i64, i32, vp, i64]
+        lib.pfe_phcx_pack.restype = C.c_int
+        lib.pfe_phcx_pack.argtypes = [vp, vp, i64, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp]
+        lib.pfe_phcx_free.restype = None
+        lib.pfe_phcx_free.argtypes = [vp]
         if path is None:
             _lib = lib
         return lib
@@ -274,3 +314,68 @@ class Engine:
         )
         self._check(self.lib.pfe_bates22(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
         return out, status
+
+
+class PhcxBatch:
+    """Files parsed by the native reader (pfe_phcx_parse): per-file info and decoded fields."""
+
+    def __init__(self, paths, mode: int = -1, threads: int = 0):
+        self.lib = load_library()
+        self.paths = [os.fsencode(p) for p in paths]
+        arr = (C.c_char_p * max(1, len(self.paths)))(*self.paths)
+        h = C.c_void_p()
+        rc = self.lib.pfe_phcx_parse(arr, len(self.paths), int(mode), int(threads), C.byref(h))
+        if rc != PFE_OK:
+            raise PfeError(f"pfe_phcx_parse failed ({rc})")
+        self._h = h
+
+    def __len__(self):
+        return len(self.paths)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.pfe_phcx_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self, i: int) -> PhcxInfo:
+        inf = PhcxInfo()
+        if self.lib.pfe_phcx_info_get(self._h, i, C.byref(inf)) != PFE_OK:
+            raise IndexError(i)
+        return inf
+
+    def fetch(self, i: int, field: int, count: int, dtype=np.uint8) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if self.lib.pfe_phcx_fetch(self._h, i, field, out.ctypes.data, count) != PFE_OK:
+            raise PfeError(f"pfe_phcx_fetch({i}, {field}) failed")
+        return out
+
+    def pack(self, rows, lp=None, ld=None, nsub_lsb=None, ndm=None, threads: int = 0):
+        """Dense arrays of the given rows (all of one shape): dict of numpy arrays."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        n = len(rows)
+        out = {"scal": np.empty((n, 8), dtype=np.float64)}
+        ptr = {}
+        if lp is not None:
+            out["prof"] = np.empty((n, lp), dtype=np.uint8)
+        if ld is not None:
+            out["lyon_dm"] = np.empty((n, ld), dtype=np.uint8)
+        if nsub_lsb is not None:
+            out["sub"] = np.empty((n,) + tuple(nsub_lsb), dtype=np.uint8)
+        if ndm is not None:
+            out["dmcurve"] = np.empty((n, ndm), dtype=np.float64)
+        for k in ("prof", "lyon_dm", "sub", "dmcurve"):
+            ptr[k] = out[k].ctypes.data if k in out else None
+        rc = self.lib.pfe_phcx_pack(
+            self._h, rows.ctypes.data, n, int(threads),
+            ptr["prof"], lp or 0, ptr["lyon_dm"], ld or 0,
+            ptr["sub"], (nsub_lsb[0] * nsub_lsb[1]) if nsub_lsb else 0,
+            ptr["dmcurve"], ndm or 0, out["scal"].ctypes.data)
+        if rc != PFE_OK:
+            raise PfeError("pfe_phcx_pack: rows of another shape or failed files")
+        return out

@@ -17,6 +17,8 @@ LIBDIR = os.path.join(HERE, "lib")
 BUILDDIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIBDIR, "libpfe.so")
 SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip"]
+HOST_SOURCES = ["phcx_io.cpp"]  # host-only C++ (PHCX reader / batch packer), built with g++
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]
 ARCH = os.environ.get("PFE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -70,6 +72,14 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
         if force or _needs(o, [s] + headers):
             jobs.append([cc, *COMMON, *extra, "-c", s, "-o", o])
 
+    cxx = shutil.which("g++") or "g++"
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(builddir, src.replace(".cpp", ".o"))
+        objs.append(o)
+        if force or _needs(o, [s] + headers + [os.path.join(HERE, "..", "include", "pfe_io.h")]):
+            jobs.append([cxx, *HOST_FLAGS, *extra, "-c", s, "-o", o])
+
     def run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -82,7 +92,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
         list(ex.map(run, jobs))
     if force or jobs or not os.path.exists(lib):
         tmp = lib + ".tmp"
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lz", "-pthread"])
         os.replace(tmp, lib)
     return lib
 

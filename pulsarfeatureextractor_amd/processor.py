@@ -47,7 +47,39 @@ def _parse_one(path):
         return None, f"{type(e).__name__}: {e}"
 
 
-def parse_all(paths, workers: int | None = None):
+def _from_native(b, i, inf, path):
+    """PHCXCandidate from a file the native reader parsed (include/pfe_io.h)."""
+    from ._native import (PFE_PHCX_DM_CURVE, PFE_PHCX_LYON_DM, PFE_PHCX_PROFILE,
+                          PFE_PHCX_SUBBANDS)
+
+    scal = np.array(inf.scal[:], dtype=np.float64)
+    return _phcx.PHCXCandidate(
+        path=path, superb=bool(inf.superb), section=inf.section,
+        profile=b.fetch(i, PFE_PHCX_PROFILE, inf.lp).astype(np.int64),
+        lyon_dm=b.fetch(i, PFE_PHCX_LYON_DM, inf.ld).astype(np.int64),
+        subbands=b.fetch(i, PFE_PHCX_SUBBANDS, inf.nsub * inf.lsb).astype(np.int64)
+        .reshape(inf.nsub, inf.lsb),
+        dm_curve=b.fetch(i, PFE_PHCX_DM_CURVE, inf.ndm, np.float64),
+        scal=scal, period_ms=scal[0], snr=scal[1], dm=scal[2], width=scal[3])
+
+
+def parse_all(paths, workers: int | None = None, native: bool = True):
+    """Parse candidate files in discovery order -> [(PHCXCandidate | None, error | None)].
+
+    native: the threaded C++ reader of libpfe.so (pfe_phcx_parse); files it flags (malformed
+    text, decoded values outside a byte, ...) are re-parsed by the Python parser so their
+    outcome, including the exception, is the reference's.  native=False: Python parser on a
+    process pool."""
+    if native and len(paths):
+        from ._native import PhcxBatch
+
+        b = PhcxBatch(paths, threads=workers or 0)
+        res = []
+        for i, p in enumerate(paths):
+            inf = b.info(i)
+            res.append((_from_native(b, i, inf, p), None) if inf.status == 0 else _parse_one(p))
+        b.close()
+        return res
     if workers is None:
         workers = min(16, os.cpu_count() or 1)
     if workers <= 1 or len(paths) < 64:
