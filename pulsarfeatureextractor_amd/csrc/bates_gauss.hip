@@ -1086,10 +1086,8 @@ static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const int L = a.lp;
   // batched lmdif (lm_batch.h) unless PFE_BLM=0 selects the wave-per-fit kernels (A/B runs)
-  static const bool use_blm = [] {
-    const char* e = getenv("PFE_BLM");
-    return !(e && e[0] == '0');
-  }();
+  const char* blm_env = getenv("PFE_BLM");
+  const bool use_blm = !(blm_env && blm_env[0] == '0');
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
     hipLaunchKernelGGL((k_ghist<P, 4, false>), gw(a.n), dim3(BLOCK), 0, st, a);         \
@@ -1109,8 +1107,10 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
     PFE_GAUSS_LAUNCH(1);
   else if (L <= 128)
     PFE_GAUSS_LAUNCH(2);
-  else
+  else if (L <= 256)
     PFE_GAUSS_LAUNCH(4);
+  else
+    PFE_GAUSS_LAUNCH(16);
 #undef PFE_GAUSS_LAUNCH
   return hipGetLastError();
 }

@@ -461,6 +461,212 @@ __global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
   }
 }
 
+// Sub-bands longer than 128 bins (up to 1024): the integer boxcar sums live in LDS
+// (NSUB x 64*SL ints: 16 KiB at 256 bins, 64 KiB at 1024) and the loops over window slots
+// stay rolled, instead of 16 x SL doubles per lane that spill; same arithmetic, in the same
+// order, as k_subband.
+template <int SL>
+__global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
+  constexpr int NSUB = 16;
+  __shared__ int bsi[NSUB][64 * SL];
+  const int64_t c = blockIdx.x;
+  if (c >= a.n) return;
+  const int lane = lane_id();
+  const int nsub = a.nsub, lsb = a.lsb;
+  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
+  const int wb = (int)ceil(width * (double)lsb);                     // :1603
+  uint32_t fail = 0;
+  if (wb <= 0 || wb > lsb) fail = PFE_ST_SUBBAND_FAIL;
+  if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;
+  if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
+  if (fail) {
+    if (lane == 0) a.status[c] |= fail;
+    return;
+  }
+  const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
+  const int nw = lsb - wb + 1;
+  double max_bin[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) max_bin[i] = 0.0;
+#pragma unroll 1
+  for (int i = 0; i < NSUB; ++i) {
+    int best = -1, bestj = 0;
+#pragma unroll 1
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      int sum = 0;
+      if (i < nsub && j < nw)
+        for (int b = 0; b < wb; ++b) sum += sb[i * lsb + j + b];
+      bsi[i][j] = sum;
+      if (i < nsub && j < nw && sum > best) {
+        best = sum;
+        bestj = j;
+      }
+    }
+    if (i < nsub) {
+      int bv = best, bj = (best >= 0) ? bestj : (1 << 30);
+#pragma unroll
+      for (int st = 1; st < 64; st <<= 1) {
+        const int ov = __shfl_xor(bv, st), oj = __shfl_xor(bj, st);
+        if (ov > bv || (ov == bv && oj < bj)) {
+          bv = ov;
+          bj = oj;
+        }
+      }
+        put(max_bin, i, (double)(bj + wb / 2));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  double msum = 0.0;
+  for (int i = 0; i < nsub; ++i) msum += max_bin[i];
+  const double med = msum / (double)nsub;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i = 0; i < nsub; ++i)
+    if (fabs(max_bin[i] - med) <= (double)wb) {
+      ++count;
+      var_med += (max_bin[i] - med) * (max_bin[i] - med);
+    }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    double mu = 0.0;
+    for (int i = 0; i < nsub; ++i) mu += max_bin[i];
+    mu /= (double)nsub;
+    var = 0.0;
+    for (int i = 0; i < nsub; ++i) var += (max_bin[i] - mu) * (max_bin[i] - mu);
+    var /= (double)(nsub - 1);
+  }
+  const double rms = sqrt(var) / (double)wb;
+  const double inv = 1.0 / (double)(nw - 1);
+  double bmean[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    double sm = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < SL; ++k) sm += (double)bsi[i][lane + 64 * k];
+    bmean[i] = sm;
+  }
+  wsum_arr(bmean);
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) bmean[i] = bmean[i] / (double)nw;
+  auto cb = [&](int i, int k) -> double {
+    const int j = lane + 64 * k;
+    return (j < nw) ? (double)bsi[i][j] - sel(bmean, i) : 0.0;
+  };
+  double var_i[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    double sm = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      const double v = (j < nw) ? (double)bsi[i][j] - bmean[i] : 0.0;
+      sm += v * v;
+    }
+    var_i[i] = sm;
+  }
+  wsum_arr(var_i);
+  double csum = 0.0;
+  int m = 0;
+#pragma unroll 1
+  for (int i = 0; i + 1 < nsub; ++i) {
+    double d[NSUB];
+#pragma unroll
+    for (int k2 = 0; k2 < NSUB; ++k2) {
+      double sm = 0.0;
+      if (k2 > i) {
+#pragma unroll 1
+        for (int k = 0; k < SL; ++k) {
+          const int j = lane + 64 * k;
+          const double v2 = (j < nw) ? (double)bsi[k2][j] - bmean[k2] : 0.0;
+          sm += cb(i, k) * v2;
+        }
+      }
+      d[k2] = sm;
+    }
+    wsum_arr(d);
+    const double vi = sel(var_i, i);
+#pragma unroll
+    for (int k2 = 0; k2 < NSUB; ++k2) {
+      if (k2 > i && k2 < nsub) {
+        const double cc = corr_from(d[k2] * inv, vi * inv, var_i[k2] * inv);
+        if (cc == cc) {
+          csum += cc;
+          ++m;
+        }
+      }
+    }
+  }
+  if (m == 0) {
+    if (lane == 0) a.status[c] |= PFE_ST_SUBBAND_FAIL;
+    return;
+  }
+  const double mean_corr = csum / (double)m;
+  double pm = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < SL; ++k) {
+    const int j = lane + 64 * k;
+    pm += (j < lsb) ? (double)a.prof[c * a.lp + j] : 0.0;
+  }
+  pm = wsum(pm) / (double)lsb;
+  auto pvk = [&](int k) -> double {
+    const int j = lane + 64 * k;
+    return (j < lsb) ? (double)a.prof[c * a.lp + j] - pm : 0.0;
+  };
+  double pvar = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < SL; ++k) {
+    const double v = pvk(k);
+    pvar += v * v;
+  }
+  pvar = wsum(pvar);
+  const double inv2 = 1.0 / (double)(lsb - 1);
+  double sv[NSUB], dv[NSUB];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    double sm = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      sm += (j < lsb && i < nsub) ? (double)sb[i * lsb + j] : 0.0;
+    }
+    sv[i] = sm;
+  }
+  wsum_arr(sv);
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i) {
+    const double mu = sv[i] / (double)lsb;
+    double dd = 0.0, q = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < SL; ++k) {
+      const int j = lane + 64 * k;
+      if (j < lsb && i < nsub) {
+        const double t = (double)sb[i * lsb + j] - mu;
+        dd += t * pvk(k);
+        q += t * t;
+      }
+    }
+    sv[i] = q;
+    dv[i] = dd;
+  }
+  wsum_arr(sv);
+  wsum_arr(dv);
+  double integ = 0.0;
+  for (int i = 0; i < nsub; ++i) {
+    const double cc = fabs(corr_from(dv[i] * inv2, sv[i] * inv2, pvar * inv2));
+    if (cc > 0.0055) integ += cc;
+  }
+  if (lane == 0) {
+    double* o = a.out + c * 22;
+    o[19] = rms;
+    o[20] = mean_corr;
+    o[21] = integ;
+  }
+}
+
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 grid_waves(int64_t n) { return grid_for_candidates(n); }
 
@@ -493,8 +699,10 @@ hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_subband<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else if (a.lsb <= 128)
     hipLaunchKernelGGL(k_subband<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+  else if (a.lsb <= 256)
+    hipLaunchKernelGGL(k_subband_lds<4>, dim3((unsigned)a.n), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL(k_subband<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL(k_subband_lds<16>, dim3((unsigned)a.n), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

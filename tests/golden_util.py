@@ -32,3 +32,38 @@ def bates_inputs(d):
     scal[:, 5] = d["dm_end"]
     scal[:, 6] = blk.shape[1]
     return d["prof"], d["sub"], curves, scal
+
+
+def oracle_with_floor(prof, sub, curve, scal):
+    """Oracle scores of a fresh batch plus that batch's own chaos floor: the fraction of
+    candidates whose score moves (> 1e-5 / > 1e-3 relative) when every leastsq start point
+    is nudged by one ulp (the tools/chaos_floor.py procedure, applied to this batch)."""
+    import warnings
+
+    import oracle.bates as B
+
+    orig = B.leastsq
+
+    def nudged(f, x0, args=(), **kw):
+        x = np.array(x0, dtype=float).copy()
+        nz = x != 0
+        x[nz] = np.nextafter(x[nz], np.inf)
+        return orig(f, x, args=args, **kw)
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a, sa = B.bates22(prof, sub, curve, scal)
+        try:
+            B.leastsq = nudged
+            b, sb = B.bates22(prof, sub, curve, scal)
+        finally:
+            B.leastsq = orig
+    ok = ((sa & 0xFF) == 0) & ((sb & 0xFF) == 0)
+    with np.errstate(all="ignore"):
+        r = np.abs(a - b) / np.maximum(np.abs(a), 1e-300)
+    r[(a == b) | (np.isnan(a) & np.isnan(b))] = 0.0
+    r[np.isnan(r)] = np.inf
+    r = r[ok]
+    floor = {"moved_1e-5": (r > 1e-5).mean(axis=0).tolist(),
+             "moved_1e-3": (r > 1e-3).mean(axis=0).tolist()}
+    return a, sa, floor

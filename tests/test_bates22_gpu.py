@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN, bates_inputs, load
+from golden_util import GOLDEN, bates_inputs, load, oracle_with_floor
 from oracle.bates import bates22 as oracle_bates22
 from pulsarfeatureextractor_amd.synth import bates_batch
 
@@ -37,19 +37,24 @@ def rel_err(got, ref):
     return r
 
 
-def check_against(out, st, ref, ref_ok, tag, floor):
+def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(), slack=0.03):
+    """close: scores held to <= 1e-12 relative (class X) instead of bit-exactness -- s20/s22
+    at lengths where numpy's BLAS dot products sum in another order than a power-of-two
+    tree (the difference is an ulp)."""
     gok = (st & 0xFF) == 0
     assert np.array_equal(gok, ref_ok), f"{tag}: failure pattern differs"
     got, ref = out[gok], ref[gok]
     r = rel_err(got, ref)
-    for j in BITEXACT:
+    for j in bitexact:
         assert (r[:, j] == 0).all(), f"{tag}: s{j + 1} not bit-exact ({(r[:, j] > 0).sum()} rows)"
+    for j in close:
+        assert (r[:, j] <= 1e-12).all(), f"{tag}: s{j + 1} max rel {r[:, j].max():.3g} > 1e-12"
     for j in range(22):
-        if j in BITEXACT:
+        if j in bitexact or j in close:
             continue
         for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3")):
             moved = (r[:, j] > tol).mean()
-            allowed = 1.5 * floor[key][j] + 0.03
+            allowed = 1.5 * floor[key][j] + slack
             assert moved <= allowed, (f"{tag}: s{j + 1} differs by > {tol} in {moved:.3f} of rows "
                                       f"(reference 1-ulp floor {floor[key][j]:.3f})")
 
@@ -67,6 +72,34 @@ def test_vs_oracle_fresh_inputs(engine):
     out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     ref, rst = oracle_bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", FLOOR["bates22_phcx128"])
+
+
+@pytest.mark.parametrize("lp,n", [(256, 96), (100, 64), (200, 48), (512, 24)])
+def test_vs_oracle_other_lengths(engine, lp, n):
+    """Config 4 (Lp = Lsb = 256), ragged lengths (MPL slots partly empty) and the long-profile
+    kernels (lp > 256: 16 rows per lane, wide histograms)."""
+    b = bates_batch(n, lp=lp, lsb=lp, seed=1000 + lp)
+    out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    ref, rst, own = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    pow2 = lp & (lp - 1) == 0
+    exact = BITEXACT if pow2 else tuple(j for j in BITEXACT if j not in (19, 21))
+    # floor: the larger of this batch's own 1-ulp floor and the 128-bin golden floor
+    gold = FLOOR["bates22_phcx128"]
+    floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
+    check_against(out, st, ref, (rst & 0xFF) == 0, f"oracle lp={lp}", floor,
+                  bitexact=exact, close=() if pow2 else (19, 21))
+
+
+def test_batched_solver_bit_identical(engine, monkeypatch):
+    """The batched lmdif kernels (lm_batch.h) reproduce the wave-per-fit kernels bit for bit
+    (PFE_BLM=0 selects the latter)."""
+    b = bates_batch(200, seed=21)
+    monkeypatch.setenv("PFE_BLM", "0")
+    o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    monkeypatch.setenv("PFE_BLM", "1")
+    o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert np.array_equal(s0, s1)
+    assert np.array_equal(np.nan_to_num(o0, nan=7.0), np.nan_to_num(o1, nan=7.0))
 
 
 def test_device_pointers_and_determinism(engine):
@@ -87,7 +120,8 @@ def test_batch_independence(engine):
     """A candidate's scores do not depend on its neighbours (shard/concat equivalence)."""
     b = bates_batch(96, seed=9)
     full, sf = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    parts = [engine.bates22(b["prof"][i:i + 32], b["sub"][i:i + 32], b["dmcurve"][i:i + 32],
-                            b["scal"][i:i + 32]) for i in range(0, 96, 32)]
-    cat = np.concatenate([p[0] for p in parts])
-    assert np.array_equal(np.nan_to_num(cat, nan=7.0), np.nan_to_num(full, nan=7.0))
+    for cuts in ((0, 32, 64, 96), (0, 7, 40, 41, 96)):  # whole and partial 32-fit batches
+        parts = [engine.bates22(b["prof"][i:j], b["sub"][i:j], b["dmcurve"][i:j], b["scal"][i:j])
+                 for i, j in zip(cuts[:-1], cuts[1:])]
+        cat = np.concatenate([p[0] for p in parts])
+        assert np.array_equal(np.nan_to_num(cat, nan=7.0), np.nan_to_num(full, nan=7.0))
