@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""End-to-end throughput of the batched ScoreGenerator path: directory of PHCX files ->
+native parse -> pfe_bates22 / pfe_lyon8 on the GPU -> score text, phase by phase.
+
+  python tools/e2e_bench.py --n 4000 [--dir /tmp/pfe_e2e] [--workers 16]
+
+The synthetic files follow SURVEY.md §8(d) (128-bin profile, 16x128 sub-bands, a
+128 x 128 DataBlock per section).  Writing them is not timed.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _write(args):
+    i, d = args
+    from pulsarfeatureextractor_amd import phcx
+    from pulsarfeatureextractor_amd.synth import bates_batch
+
+    b = bates_batch(1, seed=7000 + i)
+    rng = np.random.default_rng(i)
+    curve = b["dmcurve"][0]
+    blocks = (phcx.make_datablock(curve, rng), phcx.make_datablock(curve, rng))
+    s = b["scal"][0]
+    p = os.path.join(d, f"cand_{i:06d}.phcx.gz")
+    phcx.write(p, profile=b["prof"][0], subbands=b["sub"][0], datablocks=blocks,
+               dm_start=0.0, dm_end=200.0, n_dm_index=len(blocks[1]),
+               period_s=float(s[0]) / 1000.0, snr=float(s[1]), dm=float(s[2]), width=float(s[3]))
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=4000)
+    ap.add_argument("--dir", default="/tmp/pfe_e2e")
+    ap.add_argument("--workers", type=int, default=16)
+    args = ap.parse_args()
+    os.makedirs(args.dir, exist_ok=True)
+    have = sorted(f for f in os.listdir(args.dir) if f.endswith(".phcx.gz"))
+    if len(have) < args.n:
+        with ProcessPoolExecutor(args.workers) as ex:
+            list(ex.map(_write, [(i, args.dir) for i in range(args.n)], chunksize=64))
+    from pulsarfeatureextractor_amd import processor, writers
+    from pulsarfeatureextractor_amd.candidate import get_engine
+
+    eng = get_engine(0)
+    paths = processor.discover(args.dir, [processor.PHCX_RE])[: args.n]
+    res = {"files": len(paths)}
+    t0 = time.perf_counter()
+    parsed = processor.parse_all(paths, args.workers, native=True)
+    t1 = time.perf_counter()
+    cands = [c for c, e in parsed if c is not None]
+    sc, errs = processor.score_bates(cands, eng)
+    t2 = time.perf_counter()
+    lines = [writers.score_line(c.path, sc[j]) for j, c in enumerate(cands) if errs[j] is None]
+    t3 = time.perf_counter()
+    ly = processor.score_lyon8(cands, eng)
+    t4 = time.perf_counter()
+    res.update({
+        "parse_native_s": t1 - t0, "parse_files_per_s": len(paths) / (t1 - t0),
+        "bates22_s": t2 - t1, "bates22_cand_per_s": len(cands) / (t2 - t1),
+        "write_lines_s": t3 - t2, "lyon8_s": t4 - t3,
+        "e2e_22score_files_per_s": len(paths) / (t3 - t0),
+        "scored": len(lines), "lyon_rows": int(np.isfinite(ly[:, 0]).sum()),
+        "workers": args.workers,
+    })
+    n_py = min(200, len(paths))
+    t5 = time.perf_counter()
+    processor.parse_all(paths[:n_py], 1, native=False)
+    res["parse_python_1core_files_per_s"] = n_py / (time.perf_counter() - t5)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
