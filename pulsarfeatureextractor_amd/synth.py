@@ -105,3 +105,34 @@ def lyon_batch_torch(n: int, lp: int = 128, ld: int = 128, seed: int = BASE_SEED
         return out
 
     return rows(lp), rows(ld)
+
+
+def pfd_candidate(rng: np.random.Generator, npart: int = 8, nsub: int = 16, proflen: int = 64,
+                  pulsar: bool = True, lofreq: float = 1200.0, chan_wid: float = 1.0,
+                  chan_per_sub: int = 4):
+    """Arrays of one synthetic PRESTO fold (pfd.write keywords): noise sub-integration
+    profiles plus, for pulsar-like candidates, a pulse dispersed at the true DM, so that
+    de-dispersion at the best DM lines the sub-bands up.  The DM grid spans the best DM."""
+    f1 = rng.uniform(1.0, 20.0)  # fold frequency (Hz): bins per second = f1 * proflen
+    dm_true = rng.uniform(10.0, 150.0)
+    bestdm = dm_true + rng.normal(0.0, 0.5)
+    numchan = nsub * chan_per_sub
+    subdelta = chan_wid * chan_per_sub
+    subfreqs = np.arange(nsub) * subdelta + lofreq + subdelta - chan_wid
+    delays = dm_true / (0.000241 * subfreqs ** 2)
+    shift = (delays - delays[-1]) * f1 * proflen  # bins the pulse lags in each sub-band
+    t = np.arange(proflen)
+    profs = rng.normal(100.0, 10.0, size=(npart, nsub, proflen))
+    if pulsar:
+        mu, sig, amp = rng.uniform(0, proflen), rng.uniform(1.0, 4.0), rng.uniform(5.0, 40.0)
+        for j in range(nsub):
+            d = np.abs(t - (mu + shift[j]) % proflen)
+            d = np.minimum(d, proflen - d)
+            profs[:, j, :] += amp * np.exp(-0.5 * (d / sig) ** 2)
+    stats = np.zeros((npart, nsub, 7))
+    stats[:, :, 0] = 1000.0
+    stats[:, :, 5] = profs.var(axis=2) * rng.uniform(0.9, 1.1)
+    ndms = int(rng.integers(20, 80))
+    dms = np.linspace(bestdm - rng.uniform(5, 30), bestdm + rng.uniform(5, 30), ndms)
+    return dict(profs=profs, stats=stats, dms=dms, bestdm=bestdm, fold_p1=f1,
+                bary_p1=1.0 / f1, lofreq=lofreq, chan_wid=chan_wid, numchan=numchan)

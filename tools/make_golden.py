@@ -71,6 +71,21 @@ PATCHES = {
     ],
 }
 
+# Python-3 compatibility of the PFD reader / operations (bytes vs str) plus the Py2 integer
+# divisions the PFD path relies on
+PFD_PATCHES = {
+    "PFDFile.py": [
+        ("if test[ii] not in '0123456789:.-\\0':", "if chr(test[ii]) not in '0123456789:.-\\0':"),
+        ("self.rastr = test[:test.find('\\0')]", "self.rastr = test[:test.find(b'\\0')]"),
+        ("self.decstr = test[:test.find('\\0')]", "self.decstr = test[:test.find(b'\\0')]"),
+        ("self.chanpersub = self.numchan / self.nsub", "self.chanpersub = self.numchan // self.nsub"),
+    ],
+    "PFDOperations.py": [
+        ("dtype=Num.float)", "dtype=float)"),
+        ("shift = peak - len(profile.profile) / 2", "shift = peak - len(profile.profile) // 2"),
+    ],
+}
+
 RUNNER = r'''
 import json, sys, traceback, warnings
 warnings.simplefilter("ignore")
@@ -86,6 +101,8 @@ for f in files:
             a = list(c.calculateProfileStatScores(False))
             b = list(c.calculateDMCurveStatScores(False))
             v = [float(x) for x in a + b]
+        elif mode == "profile":
+            v = [float(x) for x in c.calculateProfileScores(False)]
         else:
             v = [float(x) for x in c.calculateScores(False)]
         res.append({"ok": True, "v": v})
@@ -104,7 +121,7 @@ def build_reference(tmp: str) -> str:
     subprocess.run([sys.executable, "-m", "lib2to3", "-f", "print", "-f", "except", "-f",
                     "has_key", "-f", "long", "-f", "numliterals", "-w", "-n", "."],
                    cwd=dst, check=True, capture_output=True)
-    for fn, subs in PATCHES.items():
+    for fn, subs in list(PATCHES.items()) + list(PFD_PATCHES.items()):
         p = os.path.join(dst, fn)
         s = open(p).read()
         for a, b in subs:
@@ -266,6 +283,69 @@ def main():
         json.dump(manifest, f, indent=1)
 
 
+PFD_SETS = [
+    # name, n, npart, nsub, proflen, base seed
+    ("pfd_64x16", 40, 8, 16, 64, 20261715),
+    ("pfd_128x32", 16, 12, 32, 128, 20261815),
+]
+
+
+def pfd_candidates(n, npart, nsub, proflen, seed):
+    """Deterministic synthetic PFD sets (regenerated from the seeds by the tests): candidate
+    i uses default_rng(seed + i); rows 0-3 are adversarial."""
+    from pulsarfeatureextractor_amd.synth import pfd_candidate
+
+    out = []
+    for i in range(n):
+        c = pfd_candidate(np.random.default_rng(seed + i), npart, nsub, proflen,
+                          pulsar=(i % 4 != 1))
+        kw = {}
+        if i == 0:
+            c["profs"][:] = 100.0          # constant: normalised profile 0/0 -> NaN
+        if i == 2:
+            kw["big_endian"] = True
+        if i == 3:
+            kw["with_posn"] = False
+        if i == 5:
+            c["dms"] = c["dms"][:1]        # numdms == 1: dms becomes a scalar, indexing raises
+        out.append((c, kw))
+    return out
+
+
+def make_pfd_golden(manifest):
+    from pulsarfeatureextractor_amd import pfd
+
+    with tempfile.TemporaryDirectory(prefix="pfe_golden_pfd_") as tmp:
+        refdir = build_reference(tmp)
+        for name, n, npart, nsub, proflen, seed in PFD_SETS:
+            d = os.path.join(tmp, name)
+            os.makedirs(d)
+            files = []
+            checks = []
+            for i, (c, kw) in enumerate(pfd_candidates(n, npart, nsub, proflen, seed)):
+                p = os.path.join(d, f"{name}_{i:04d}.pfd")
+                pfd.write(p, **c, **kw)
+                files.append(p)
+                checks.append(float(np.asarray(c["profs"]).sum()))
+            arrs = {}
+            for mode, nout in (("lyon8", 8), ("profile", proflen), ("bates22", 22)):
+                res = run_reference(refdir, files, mode, tmp)
+                out, ok, errs = collect(res, nout)
+                arrs[mode] = (out, ok, errs)
+                print(f"{name} {mode}: {int((~ok).sum())} reference failures", flush=True)
+            np.savez_compressed(
+                os.path.join(GOLDEN, name + ".npz"), n=n, npart=npart, nsub=nsub,
+                proflen=proflen, seed=seed, profs_sum=np.array(checks),
+                lyon8=arrs["lyon8"][0], lyon8_ok=arrs["lyon8"][1], lyon8_err=arrs["lyon8"][2],
+                profile=arrs["profile"][0], profile_ok=arrs["profile"][1],
+                bates22=arrs["bates22"][0], bates22_ok=arrs["bates22"][1],
+                bates22_err=arrs["bates22"][2])
+            manifest["sets"][name] = {"mode": "pfd lyon8 + profile + bates22", "n": n,
+                                      "npart": npart, "nsub": nsub, "proflen": proflen,
+                                      "seed": seed, "generator": "synth.pfd_candidate",
+                                      "patches": {k: [a for a, _ in v] for k, v in PFD_PATCHES.items()}}
+
+
 def _rows_lyon(rng, n, L):
     from pulsarfeatureextractor_amd.synth import _rows_numpy
 
@@ -273,4 +353,11 @@ def _rows_lyon(rng, n, L):
 
 
 if __name__ == "__main__":
-    main()
+    if "--pfd" in sys.argv:  # only the PFD sets (the PHCX sets are unchanged)
+        mpath = os.path.join(GOLDEN, "manifest.json")
+        man = json.load(open(mpath))
+        make_pfd_golden(man)
+        with open(mpath, "w") as f:
+            json.dump(man, f, indent=1)
+    else:
+        main()
