@@ -143,6 +143,41 @@ typedef struct pfe_bates_in {
 int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
                 uint32_t flags);
 
+/* ---- PFD (PRESTO fold) files: preprocessing + Lyon features -------------------------
+ * pfe_pfd_dmprof <- what a freshly loaded PFDFile computes for the dmprof path
+ *   dedisperse (PFDFile.py:330-374) at the best DM, getprofile + scale (:256-310),
+ *   plot_chi2_vs_DM(dms[0], dms[-1]) (:378-423, 100 DMs, float32),
+ *   computeProfileStatScores (:522-551) and computeDMCurveStatScores (:553-583).
+ * Inputs per candidate: the fold's sub-integration profiles profs[npart][nsub][proflen],
+ * the sub-band centre frequencies (PFDFile.py:222-226) and the scalars below (from the
+ * file header: best DM, fold_p1 * proflen, (profs/proflen).sum() of the file as read,
+ * the summed prof_var foldstats, dms[0], dms[-1] and numdms).
+ * Outputs (each may be NULL): profile[n][proflen] (0..255 fp64, also the --profile bins of
+ * PFDFile.computeProfileScores :479-492), chis[n][PFE_PFD_NDM] (the float32 DM curve),
+ * lyon8[n][8] = [profile mean, std, skew, kurt, DM-curve mean, std, skew, kurt].
+ * status[i] = PFE_ST_PFD_DMCURVE_FAIL when numdms == 1 (the reference raises on dms[0]). */
+#define PFE_PFD_NSCAL 8
+#define PFE_PFD_BESTDM 0
+#define PFE_PFD_BINSPERSEC 1
+#define PFE_PFD_AVGPROF 2
+#define PFE_PFD_VARPROF 3
+#define PFE_PFD_DM_LO 4
+#define PFE_PFD_DM_HI 5
+#define PFE_PFD_NUMDMS 6
+#define PFE_PFD_NDM 100
+#define PFE_ST_PFD_DMCURVE_FAIL 0x020u
+
+typedef struct pfe_pfd_in {
+  const double* profs;    /* n x npart x nsub x proflen */
+  const double* subfreqs; /* n x nsub */
+  const double* scal;     /* n x PFE_PFD_NSCAL */
+  int32_t npart, nsub, proflen;
+  int64_t n;
+} pfe_pfd_in;
+
+int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* chis,
+                   double* lyon8, uint32_t* status, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

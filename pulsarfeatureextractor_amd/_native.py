@@ -37,7 +37,11 @@ EXPORTED_SYMBOLS = (
     "pfe_lyon8_u8",
     "pfe_lyon8_f64",
     "pfe_bates22",
+    "pfe_pfd_dmprof",
 )
+PFE_PFD_NSCAL = 8
+PFE_PFD_NDM = 100
+PFE_ST_PFD_DMCURVE_FAIL = 0x020
 # every symbol include/pfe_io.h declares
 EXPORTED_IO_SYMBOLS = (
     "pfe_phcx_parse",
@@ -65,6 +69,18 @@ class BatesIn(C.Structure):
         ("dmcurve", C.c_void_p),
         ("ndm", C.c_int32),
         ("scal", C.c_void_p),
+        ("n", C.c_int64),
+    ]
+
+
+class PfdIn(C.Structure):
+    _fields_ = [
+        ("profs", C.c_void_p),
+        ("subfreqs", C.c_void_p),
+        ("scal", C.c_void_p),
+        ("npart", C.c_int32),
+        ("nsub", C.c_int32),
+        ("proflen", C.c_int32),
         ("n", C.c_int64),
     ]
 
@@ -146,6 +162,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_lyon8_f64.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
         lib.pfe_bates22.restype = C.c_int
         lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
+        lib.pfe_pfd_dmprof.restype = C.c_int
+        lib.pfe_pfd_dmprof.argtypes = [vp, C.POINTER(PfdIn), vp, vp, vp, vp, u32]
         pp = C.POINTER(C.c_char_p)
         lib.pfe_phcx_parse.restype = C.c_int
         lib.pfe_phcx_parse.argtypes = [pp, i64, i32, i32, C.POINTER(vp)]
@@ -314,6 +332,43 @@ class Engine:
         )
         self._check(self.lib.pfe_bates22(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
         return out, status
+
+    def pfd_dmprof(self, profs, subfreqs, scal, profile=True, chis=True, lyon8=True):
+        """PFD preprocessing + Lyon features (pfe_pfd_dmprof) for a batch of folds of one
+        shape: profs (n,npart,nsub,L) f64, subfreqs (n,nsub), scal (n,PFE_PFD_NSCAL).
+        Returns dict(profile (n,L) f64, chis (n,100) f32, lyon8 (n,8) f64, status (n,))."""
+        n, npart, nsub, L = profs.shape
+        if subfreqs.shape != (n, nsub) or scal.shape != (n, PFE_PFD_NSCAL):
+            raise ValueError("pfd_dmprof: subfreqs must be (n,nsub), scal (n,%d)" % PFE_PFD_NSCAL)
+        dev = _is_device(profs)
+        out = {}
+        if dev:
+            import torch
+
+            self._follow_torch()
+            mk = lambda shape, dt: torch.empty(shape, dtype=dt, device=profs.device)  # noqa: E731
+            f64, f32, i32 = torch.float64, torch.float32, torch.int32
+            for t in (profs, subfreqs, scal):
+                if not t.is_contiguous():
+                    raise ValueError("pfd_dmprof: device tensors must be contiguous")
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            profs = np.ascontiguousarray(profs, dtype=np.float64)
+            subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
+            scal = np.ascontiguousarray(scal, dtype=np.float64)
+            mk = lambda shape, dt: np.empty(shape, dtype=dt)  # noqa: E731
+            f64, f32, i32 = np.float64, np.float32, np.uint32
+            flags = 0
+        out["profile"] = mk((n, L), f64) if profile else None
+        out["chis"] = mk((n, PFE_PFD_NDM), f32) if chis else None
+        out["lyon8"] = mk((n, 8), f64) if lyon8 else None
+        out["status"] = mk((n,), i32)
+        pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
+        self._check(self.lib.pfe_pfd_dmprof(
+            self._h, C.byref(pin), _ptr(out["profile"]) if profile else None,
+            _ptr(out["chis"]) if chis else None, _ptr(out["lyon8"]) if lyon8 else None,
+            _ptr(out["status"]), flags))
+        return out
 
 
 class PhcxBatch:

@@ -13,6 +13,7 @@
 #include <string>
 
 #include "../../include/pfe.h"
+#include "pfd.h"
 
 namespace pfe {
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
@@ -274,6 +275,87 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipStreamSynchronize(st));
+  }
+  return PFE_OK;
+}
+
+int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* chis,
+                   double* lyon8, uint32_t* status, uint32_t flags) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  if (!in || !status) return set_err(h, PFE_EINVAL, "pfd_dmprof: null argument");
+  const int64_t n = in->n;
+  if (n < 0) return set_err(h, PFE_EINVAL, "pfd_dmprof: n < 0");
+  if (n == 0) return PFE_OK;
+  if (!in->profs || !in->subfreqs || !in->scal)
+    return set_err(h, PFE_EINVAL, "pfd_dmprof: null input array");
+  if (in->npart < 1 || in->nsub < 1 || in->proflen < 2)
+    return set_err(h, PFE_EINVAL, "pfd_dmprof: shape %dx%dx%d", in->npart, in->nsub, in->proflen);
+  if (pfe::pfd_lds_bytes(in->nsub, in->proflen) > 160 * 1024)
+    return set_err(h, PFE_EINVAL, "pfd_dmprof: nsub*proflen=%d exceeds the LDS-resident limit",
+                   in->nsub * in->proflen);
+  PFE_HIP(h, hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  pfe::PfdArgs a;
+  a.npart = in->npart;
+  a.nsub = in->nsub;
+  a.L = in->proflen;
+  a.n = n;
+  const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
+  if (flags & PFE_FLAG_DEVICE_PTRS) {
+    a.profs = in->profs;
+    a.subfreqs = in->subfreqs;
+    a.scal = in->scal;
+    a.profile = profile;
+    a.chis = chis;
+    a.lyon8 = lyon8;
+    a.status = status;
+  } else {
+    const size_t pb = align256(np * sizeof(double));
+    const size_t fb = align256((size_t)n * in->nsub * sizeof(double));
+    const size_t cb = align256((size_t)n * PFE_PFD_NSCAL * sizeof(double));
+    const size_t ob = profile ? align256((size_t)n * in->proflen * sizeof(double)) : 0;
+    const size_t xb = chis ? align256((size_t)n * PFE_PFD_NDM * sizeof(float)) : 0;
+    const size_t lb = lyon8 ? align256((size_t)n * 8 * sizeof(double)) : 0;
+    const size_t tb = align256((size_t)n * sizeof(uint32_t));
+    int rc = ensure_scratch(h, pb + fb + cb + ob + xb + lb + tb);
+    if (rc) return rc;
+    char* base = (char*)h->scratch;
+    size_t off = 0;
+    PFE_HIP(h, hipMemcpyAsync(base, in->profs, np * sizeof(double), hipMemcpyHostToDevice, st));
+    a.profs = (const double*)base;
+    off += pb;
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->subfreqs, (size_t)n * in->nsub * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    a.subfreqs = (const double*)(base + off);
+    off += fb;
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->scal, (size_t)n * PFE_PFD_NSCAL * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    a.scal = (const double*)(base + off);
+    off += cb;
+    a.profile = profile ? (double*)(base + off) : nullptr;
+    off += ob;
+    a.chis = chis ? (float*)(base + off) : nullptr;
+    off += xb;
+    a.lyon8 = lyon8 ? (double*)(base + off) : nullptr;
+    off += lb;
+    a.status = (uint32_t*)(base + off);
+  }
+  hipError_t e = pfe::launch_pfd_dmprof(a, st);
+  if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "pfd_dmprof launch: %s", hipGetErrorString(e));
+  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
+    if (profile)
+      PFE_HIP(h, hipMemcpyAsync(profile, a.profile, (size_t)n * in->proflen * sizeof(double),
+                                hipMemcpyDeviceToHost, st));
+    if (chis)
+      PFE_HIP(h, hipMemcpyAsync(chis, a.chis, (size_t)n * PFE_PFD_NDM * sizeof(float),
+                                hipMemcpyDeviceToHost, st));
+    if (lyon8)
+      PFE_HIP(h, hipMemcpyAsync(lyon8, a.lyon8, (size_t)n * 8 * sizeof(double),
+                                hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipMemcpyAsync(status, a.status, (size_t)n * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipStreamSynchronize(st));
   }
   return PFE_OK;

@@ -150,3 +150,18 @@ def write(path: str, *, profs, stats=None, dms, bestdm, fold_p1, bary_p1=None, l
     out.append(np.asarray(stats, dtype=np.float64).astype(np.dtype(np.float64).newbyteorder(sw)).tobytes())
     with open(path, "wb") as f:
         f.write(b"".join(out))
+
+
+def batch_inputs(datas):
+    """Dense pfe_pfd_dmprof inputs for PFDData of one (npart, nsub, proflen) shape."""
+    n = len(datas)
+    d0 = datas[0]
+    profs = np.empty((n, d0.npart, d0.nsub, d0.proflen), dtype=np.float64)
+    subfreqs = np.empty((n, d0.nsub), dtype=np.float64)
+    scal = np.zeros((n, 8), dtype=np.float64)
+    for i, d in enumerate(datas):
+        profs[i] = d.profs
+        subfreqs[i] = d.subfreqs
+        dms = np.atleast_1d(d.dms)
+        scal[i, :7] = (d.bestdm, d.binspersec, d.avgprof, d.varprof, dms[0], dms[-1], d.numdms)
+    return profs, subfreqs, scal

@@ -1,0 +1,84 @@
+"""GPU parity of pfe_pfd_dmprof (PFD preprocessing + PFD Lyon features) against the
+reference's own outputs (tests/golden/pfd_*.npz) and the CPU restatement (oracle/pfd.py).
+
+Bar: the 0..255 profile (PFDFile.getprofile, also the --profile bins) bit-exact; the DM curve
+(float32 chi^2 vs DM) bit-exact against the restatement; profile mean / std / kurtosis and
+DM-curve mean / std / kurtosis bit-exact; the two skews go through pow(m2, 1.5) (libm on the
+host, the device's pow here), so they are held to 1e-13 (float64) and 1e-6 (float32)
+relative; numdms == 1 files fail exactly where the reference raises."""
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import pfd as opfd
+from pulsarfeatureextractor_amd import pfd
+from test_oracle_pfd import SETS, build_files, load_set
+
+pytestmark = pytest.mark.gpu
+
+
+def run(engine, files):
+    datas = [pfd.read(f) for f in files]
+    profs, subfreqs, scal = pfd.batch_inputs(datas)
+    return datas, engine.pfd_dmprof(profs, subfreqs, scal)
+
+
+def eq_nan(a, b):
+    return (a == b) | (np.isnan(a) & np.isnan(b))
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_vs_reference(engine, tmp_path, name):
+    g = load_set(name)
+    files = build_files(tmp_path, g)
+    datas, r = run(engine, files)
+    assert eq_nan(r["profile"], g["profile"]).all(), "profile not bit-exact"
+    ok = g["lyon8_ok"]
+    assert np.array_equal((r["status"] & 0x20) == 0, ok)
+    got, ref = r["lyon8"][ok], g["lyon8"][ok]
+    for j in (0, 1, 3, 4, 5, 7):
+        assert eq_nan(got[:, j], ref[:, j]).all(), f"feature {j} not bit-exact"
+    for j, tol in ((2, 1e-13), (6, 1e-6)):
+        with np.errstate(invalid="ignore"):
+            rel = np.abs(got[:, j] - ref[:, j]) / np.abs(ref[:, j])
+        rel[eq_nan(got[:, j], ref[:, j])] = 0.0
+        assert (rel <= tol).all(), f"feature {j}: max rel {np.nanmax(rel):.3g}"
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_dm_curve_vs_oracle(engine, tmp_path, name):
+    g = load_set(name)
+    files = build_files(tmp_path, g)
+    datas, r = run(engine, files)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i, d in enumerate(datas):
+            if not g["lyon8_ok"][i]:
+                continue
+            chis = opfd.dm_curve(d)
+            assert np.array_equal(r["chis"][i], chis) or eq_nan(r["chis"][i], chis).all(), i
+
+
+def test_fresh_shapes_vs_oracle(engine, tmp_path):
+    """Other fold shapes (long profiles: pairwise sums over several 128-blocks)."""
+    from pulsarfeatureextractor_amd.synth import pfd_candidate
+
+    for npart, nsub, L in ((4, 8, 256), (6, 64, 96), (2, 3, 300)):
+        files = []
+        for i in range(4):
+            c = pfd_candidate(np.random.default_rng(500 + i + L), npart, nsub, L)
+            p = os.path.join(tmp_path, f"f{L}_{i}.pfd")
+            pfd.write(p, **c)
+            files.append(p)
+        datas, r = run(engine, files)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for i, d in enumerate(datas):
+                st = opfd.PFDState(d)
+                assert eq_nan(r["profile"][i], st.profile()).all(), (L, i)
+                ref = np.array(opfd.lyon8_one(d))
+                got = r["lyon8"][i]
+                for j in (0, 1, 3, 4, 5, 7):
+                    assert eq_nan(got[j], ref[j]), (L, i, j, got[j], ref[j])
