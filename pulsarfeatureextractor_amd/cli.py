@@ -3,8 +3,9 @@
   python -m pulsarfeatureextractor_amd.cli -c <dir|file> -o <out> [--phcx|--superb]
          [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K]
 
-Same flags, same output-file probing (:147-160), same mode dispatch (:219-290).  --pfd and
---label are recognised and rejected (PFD is a 'next' row, labelling is interactive).
+Same flags, same output-file probing (:147-160), same mode dispatch (:215-290).  PFD files
+are served in --dmprof and --profile modes; the PFD 22-score modes and --label (interactive
+labelling) are recognised and refused with exit status 2.
 """
 from __future__ import annotations
 
@@ -30,9 +31,6 @@ def main(argv=None):
     p.add_option("--device", action="store", dest="device", type="int", default=0)
     p.add_option("--workers", action="store", dest="workers", type="int", default=None)
     args, _ = p.parse_args(argv)
-    if args.pfd:
-        print("PFD candidates are not supported by this build.", file=sys.stderr)
-        return 2
     if args.label:
         print("--label (interactive labelling) is not supported by this build.", file=sys.stderr)
         return 2
@@ -56,22 +54,47 @@ def main(argv=None):
 
     get_engine(args.device)
     dp = processor.DataProcessor(args.verbose, workers=args.workers)
-    if args.dmprof:
-        if args.phcx and not args.superb:
-            dp.dmprofPHCX(search, args.verbose, args.outputPath, args.arff, single)
-        elif args.superb and not args.phcx:
-            dp.dmprofSUPERB(search, args.verbose, args.outputPath, args.arff, single)
-    elif args.phcx and not args.superb:
-        if not single_file:
-            dp.processPHCXSeparately(search, args.verbose, single)
+    phcx, pfd, superb = args.phcx, args.pfd, args.superb
+    try:
+        if args.dmprof:
+            if phcx and not pfd and not superb:
+                dp.dmprofPHCX(search, args.verbose, args.outputPath, args.arff, single)
+            elif not phcx and pfd and not superb:
+                dp.dmprofPFD(search, args.verbose, args.outputPath, args.arff, single)
+            elif not phcx and not pfd and superb:
+                dp.dmprofSUPERB(search, args.verbose, args.outputPath, args.arff, single)
+        elif phcx and not pfd and not superb:
+            if not single_file:
+                dp.processPHCXSeparately(search, args.verbose, single)
+            else:
+                dp.processPHCXCollectively(search, args.verbose, args.outputPath, args.arff,
+                                           args.profile, single)
+        elif not phcx and pfd and not superb:
+            if not single_file:
+                dp.processPFDSeparately(search, args.verbose, single)
+            else:
+                dp.processPFDCollectively(search, args.verbose, args.outputPath, args.arff,
+                                          args.profile, single)
+        elif phcx and pfd and not superb:
+            if not single_file:
+                dp.processPFDAndPHCXSeparately(search, args.verbose, single)
+            else:
+                dp.processPFDAndPHCXCollectively(search, args.verbose, args.outputPath,
+                                                 args.arff, args.profile, single)
+        elif superb and not pfd and not phcx:
+            dp.processSUPERBCollectively(search, args.verbose, args.outputPath, args.arff,
+                                         args.profile, single)
+        elif not phcx and not pfd:
+            if not single_file:
+                dp.processPFDAndPHCXSeparately(search, args.verbose, single)
+            else:
+                dp.processPFDAndPHCXCollectively(search, args.verbose, args.outputPath,
+                                                 args.arff, args.profile, single)
         else:
-            dp.processPHCXCollectively(search, args.verbose, args.outputPath, args.arff,
-                                       args.profile, single)
-    elif args.superb and not args.phcx:
-        dp.processSUPERBCollectively(search, args.verbose, args.outputPath, args.arff,
-                                     args.profile, single)
-    else:
-        print("Didn't know what to do with your input.")
+            print("Didn't know what to do with your input.")
+    except NotImplementedError as e:
+        print(f"not supported by this build: {e}", file=sys.stderr)
+        return 2
     print("Done.")
     return 0
 

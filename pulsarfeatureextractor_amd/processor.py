@@ -9,8 +9,9 @@ packed into dense arrays and scored in large batches on the GPU through libpfe.
   processPHCXCollectively / processSUPERBCollectively  (:109-146, :451-599)
   processPHCXSeparately                                (:91-105, :603-687)
   dmprofPHCX / dmprofSUPERB                            (:255-301, :830-994)
-PFD modes are not part of this build; --label is interactive and out of
-scope.
+PFD files (".pfd" in the name, Candidate.py:136) are read by pfd.read and go through
+pfe_pfd_dmprof (dmprof and profile-bin modes); the PFD 22-score path is not in this build
+yet and raises.  --label is interactive and out of scope.
 """
 from __future__ import annotations
 
@@ -21,6 +22,7 @@ from concurrent.futures import ProcessPoolExecutor
 
 import numpy as np
 
+from . import pfd as _pfd
 from . import phcx as _phcx
 from . import writers
 from .candidate import get_engine, status_error
@@ -88,6 +90,42 @@ def parse_all(paths, workers: int | None = None, native: bool = True):
         return list(ex.map(_parse_one, paths, chunksize=64))
 
 
+def is_pfd(path: str) -> bool:
+    return ".pfd" in path  # Candidate.py:136-138
+
+
+def _read_pfd(path):
+    try:
+        return _pfd.read(path), None
+    except Exception as e:  # the reference logs and skips unreadable candidates
+        return None, f"{type(e).__name__}: {e}"
+
+
+def score_pfd(datas, engine=None, batch: int = 1 << 14):
+    """PFD preprocessing + Lyon features on the GPU for parsed folds:
+    returns (lyon8 (n,8), profiles [n arrays], errors [n])."""
+    engine = engine or get_engine()
+    n = len(datas)
+    out = np.full((n, 8), np.nan)
+    profiles = [None] * n
+    err = [None] * n
+    groups: dict = {}
+    for i, d in enumerate(datas):
+        groups.setdefault((d.npart, d.nsub, d.proflen), []).append(i)
+    for _shape, idx in groups.items():
+        for s0 in range(0, len(idx), batch):
+            part = idx[s0:s0 + batch]
+            profs, subfreqs, scal = _pfd.batch_inputs([datas[i] for i in part])
+            r = engine.pfd_dmprof(profs, subfreqs, scal, chis=False)
+            for j, i in enumerate(part):
+                profiles[i] = r["profile"][j]
+                if int(r["status"][j]) & 0x20:
+                    err[i] = "Exception: DM curve stat score extraction exception"
+                else:
+                    out[i] = r["lyon8"][j]
+    return out, profiles, err
+
+
 def _shape_key(c):
     return (len(c.profile), c.subbands.shape[0], c.subbands.shape[1], len(c.dm_curve))
 
@@ -149,6 +187,7 @@ class DataProcessor:
         self.candidateErrorLog = "CandidateErrorLog.txt"
         self.superb = False
         self.phcx = False
+        self.pfd = False
         if not os.path.exists(self.candidateErrorLog):       # :86-87
             writers.append_text(self.candidateErrorLog, "")
 
@@ -183,6 +222,11 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
+        if any(is_pfd(p) for p in paths):
+            if not genProfileData:
+                raise NotImplementedError("the 22-score path for PFD files is not in this build "
+                                          "(pfe_pfd_dmprof covers --dmprof and --profile)")
+            return self._pfd_profiles(paths, outPath, arff, start)
         parsed = parse_all(paths, self.workers)
         good = [i for i, (c, e) in enumerate(parsed) if c is not None]
         cands = [parsed[i][0] for i in good]
@@ -207,6 +251,29 @@ class DataProcessor:
             self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
             ok += 1
         self._finish(outPath, len(paths), ok, failed, start)
+
+    def _pfd_profiles(self, paths, outPath, arff, start):
+        """--profile for PFD files: the 0..255 profile bins (PFDFile.computeProfileScores)."""
+        rd = [_read_pfd(p) for p in paths]
+        good = [k for k, (d, e) in enumerate(rd) if d is not None]
+        _f, profiles, _e = score_pfd([rd[k][0] for k in good], self.engine)
+        prof = {k: profiles[j] for j, k in enumerate(good)}
+        ok = failed = 0
+        for i, p in enumerate(paths):
+            if i not in prof:
+                self._fail(p, rd[i][1])
+                failed += 1
+                continue
+            s = [float(v) for v in prof[i]]
+            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
+            ok += 1
+        self._finish(outPath, len(paths), ok, failed, start)
+
+    def processPFDCollectively(self, directory, verbose, outPath, arff, genProfileData,
+                               processSingleCandidate):
+        self.pfd = True
+        self.processCollectively(directory, verbose, list(PFD_RES), outPath, arff, genProfileData,
+                                 processSingleCandidate)
 
     def processPHCXCollectively(self, directory, verbose, outPath, arff, genProfileData,
                                 processSingleCandidate):
@@ -245,20 +312,50 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        parsed = parse_all(paths, self.workers)
-        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
-        feats = score_lyon8([parsed[i][0] for i in good], self.engine)
-        row = {i: feats[j] for j, i in enumerate(good)}
+        row, why = self._lyon_rows(paths)
         ok = failed = 0
         for i, p in enumerate(paths):
             if i not in row:
-                self._fail(p, parsed[i][1])
+                self._fail(p, why.get(i))
                 failed += 1
                 continue
             s = row[i]
             self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
             ok += 1
         self._finish(outPath, len(paths), ok, failed, start)
+
+    def _lyon_rows(self, paths):
+        """{index: 8 features} for the files that score, {index: error} for the rest; PHCX /
+        SUPERB files through pfe_lyon8_u8, PFD files through pfe_pfd_dmprof."""
+        row, why = {}, {}
+        px = [i for i, p in enumerate(paths) if not is_pfd(p)]
+        pf = [i for i, p in enumerate(paths) if is_pfd(p)]
+        if px:
+            parsed = parse_all([paths[i] for i in px], self.workers)
+            good = [k for k, (c, e) in enumerate(parsed) if c is not None]
+            feats = score_lyon8([parsed[k][0] for k in good], self.engine)
+            for j, k in enumerate(good):
+                row[px[k]] = feats[j]
+            for k, (c, e) in enumerate(parsed):
+                if c is None:
+                    why[px[k]] = e
+        if pf:
+            rd = [_read_pfd(paths[i]) for i in pf]
+            good = [k for k, (d, e) in enumerate(rd) if d is not None]
+            feats, _prof, errs = score_pfd([rd[k][0] for k in good], self.engine)
+            for j, k in enumerate(good):
+                if errs[j]:
+                    why[pf[k]] = errs[j]
+                else:
+                    row[pf[k]] = feats[j]
+            for k, (d, e) in enumerate(rd):
+                if d is None:
+                    why[pf[k]] = e
+        return row, why
+
+    def dmprofPFD(self, directory, verbose, outPath, arff, processSingleCandidate):
+        self.pfd = True
+        self.dmprof(directory, verbose, list(PFD_RES), outPath, arff, processSingleCandidate)
 
     def dmprofPHCX(self, directory, verbose, outPath, arff, processSingleCandidate):
         self.phcx = True
@@ -270,9 +367,8 @@ class DataProcessor:
 
     # ---- not in this build -------------------------------------------------------------
     def _pfd(self, *a, **k):
-        raise NotImplementedError("PFD candidates are not supported by this build "
-                                  "(SURVEY.md §8(f) 'next' row)")
+        raise NotImplementedError("the PFD 22-score modes are not in this build yet "
+                                  "(--dmprof and --profile are)")
 
-    processPFDSeparately = processPFDCollectively = dmprofPFD = _pfd
-    processPFDAndPHCXSeparately = processPFDAndPHCXCollectively = _pfd
+    processPFDSeparately = processPFDAndPHCXSeparately = processPFDAndPHCXCollectively = _pfd
     labelPHCX = labelPFD = _pfd

@@ -78,3 +78,40 @@ def test_bates_cli_and_error_log(tmp_path, monkeypatch):
         ref = np.nan_to_num(d["out"][i], nan=0.0, posinf=0.0)
         for j in (2, 3, 11, 12, 13, 14, 15, 19, 21):   # bit-exact score columns
             assert got[j] == float("%.12g" % ref[j]), (i, j, got[j], ref[j])
+
+
+def test_pfd_dmprof_and_profile_cli(tmp_path, monkeypatch):
+    """--pfd --dmprof and --pfd --profile against the reference's PFD outputs."""
+    from test_oracle_pfd import build_files, load_set
+
+    monkeypatch.chdir(tmp_path)
+    g = load_set("pfd_64x16")
+    cand = tmp_path / "pfds"
+    cand.mkdir()
+    files = build_files(str(cand), g)
+    out = str(tmp_path / "dmprof.csv")
+    assert cli.main(["-c", str(cand), "-o", out, "--pfd", "--dmprof"]) == 0
+    rows = read_rows(out)
+    assert len(rows) == int(g["lyon8_ok"].sum())
+    logged = [ln for ln in open("CandidateErrorLog.txt").read().splitlines() if ln]
+    assert len(logged) == int((~g["lyon8_ok"]).sum())
+    base = str(cand) + "/"
+    for i, f in enumerate(files):
+        key = os.path.join(base, os.path.basename(f))
+        if not g["lyon8_ok"][i]:
+            assert key not in rows
+            continue
+        ref = np.nan_to_num(g["lyon8"][i], nan=0.0)
+        r = np.array([float("%.12g" % v) for v in ref])
+        # the float32 DM-curve skew goes through powf: within 1e-6 (test_pfd_gpu.py)
+        rtol = np.array([1e-11] * 6 + [1e-6, 1e-11])
+        assert (np.abs(np.array(rows[key]) - r) <= rtol * np.abs(r) + 1e-12).all(), (i, rows[key], r)
+    out2 = str(tmp_path / "prof.csv")
+    assert cli.main(["-c", str(cand), "-o", out2, "--pfd", "--profile"]) == 0
+    rows = read_rows(out2)
+    for i, f in enumerate(files):
+        ref = np.nan_to_num(g["profile"][i], nan=0.0)
+        got = rows[os.path.join(base, os.path.basename(f))]
+        assert got == [float("%.12g" % v) for v in ref], i
+    # the PFD 22-score mode is refused, not approximated
+    assert cli.main(["-c", str(cand), "-o", str(tmp_path / "s.csv"), "--pfd"]) == 2
