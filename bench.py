@@ -46,7 +46,8 @@ def parse():
                     help="candidates per GPU (default 10M for lyon8, 1M for bates22)")
     ap.add_argument("--lp", type=int, default=128)
     ap.add_argument("--ld", type=int, default=128)
-    ap.add_argument("--path", choices=["lyon8", "bates22"], default="lyon8")
+    ap.add_argument("--path", choices=["lyon8", "bates22", "pfd"], default="lyon8")
+    ap.add_argument("--pfd-shape", default="16x32x128", help="npart x nsub x proflen (pfd path)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -118,6 +119,50 @@ def cpu_baseline_bates22(lp, sample):
     }
 
 
+def pfd_block(n, shape, seed):
+    """n synthetic PRESTO folds of one shape -> pfe_pfd_dmprof inputs (numpy)."""
+    import numpy as np
+
+    from pulsarfeatureextractor_amd import pfd as _pfd
+    from pulsarfeatureextractor_amd.synth import pfd_candidate
+
+    npart, nsub, L = shape
+    datas = []
+    for i in range(n):
+        c = pfd_candidate(np.random.default_rng(seed + i), npart, nsub, L)
+        chanpersub = c["numchan"] // nsub
+        sd = c["chan_wid"] * chanpersub
+        stats = c["stats"]
+        datas.append(_pfd.PFDData(
+            npart=npart, nsub=nsub, proflen=L, profs=c["profs"], bestdm=c["bestdm"],
+            binspersec=c["fold_p1"] * L, avgprof=(c["profs"] / L).sum(),
+            varprof=float(stats[:, :, 5].sum()), dms=c["dms"], numdms=len(c["dms"]),
+            subfreqs=np.arange(nsub, dtype="d") * sd + (c["lofreq"] + sd - c["chan_wid"])))
+    return datas
+
+
+def cpu_baseline_pfd(shape, sample):
+    import warnings
+
+    from oracle.pfd import lyon8_one
+
+    datas = pfd_block(sample, shape, 4244)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        lyon8_one(datas[0])
+        t0 = time.perf_counter()
+        for d in datas:
+            lyon8_one(d)
+        dt = time.perf_counter() - t0
+    return {
+        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
+        "sample": f"{sample} synthetic {shape[0]}x{shape[1]}x{shape[2]} PRESTO folds through "
+                  f"the reference-equivalent numpy/scipy dedisperse + getprofile + "
+                  f"plot_chi2_vs_DM + stats restatement (oracle.pfd.lyon8_one), {dt:.1f} s on "
+                  f"1 host core",
+    }
+
+
 def load_ops_per_candidate():
     p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
     try:
@@ -130,9 +175,10 @@ def load_ops_per_candidate():
 def main():
     args = parse()
     if args.n is None:
-        args.n = 10_000_000 if args.path == "lyon8" else 1_000_000
+        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "pfd": 32768}[args.path]
     if args.cpu_sample is None:
-        args.cpu_sample = 8000 if args.path == "lyon8" else 300
+        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "pfd": 200}[args.path]
+    pfd_shape = tuple(int(v) for v in args.pfd_shape.split("x"))
     import torch
     import torch.distributed as dist
 
@@ -164,6 +210,24 @@ def main():
 
         def step():
             eng.lyon8(prof, dm, out=out)
+    elif args.path == "pfd":
+        import numpy as np
+
+        from pulsarfeatureextractor_amd import pfd as _pfd
+
+        blk = 1024  # synthetic folds generated on the host, tiled to n rows in HBM
+        profs, subfreqs, pscal = _pfd.batch_inputs(pfd_block(blk, pfd_shape, 20261019 + rank))
+        reps = (n + blk - 1) // blk
+
+        def tile(a):
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+            return t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
+
+        tp, tf, ts = tile(profs), tile(subfreqs), tile(pscal)
+        del profs
+
+        def step():
+            eng.pfd_dmprof(tp, tf, ts, profile=False, chis=False, lyon8=True)
     else:
         import numpy as np
 
@@ -254,6 +318,35 @@ def main():
                 "avg_kernel_ms_max_over_ranks": kern_ms_max,
             },
         }
+    elif args.path == "pfd":
+        npart, nsub, L = pfd_shape
+        bytes_per_launch = n * (npart * nsub * L * 8 + nsub * 8 + 8 * 8 + 8 * 8 + 4)
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        result = {
+            "metric": "candidates/sec (PFD dmprof path)",
+            **common,
+            "dtype": "f64 (DM-curve statistics f32, as numpy)",
+            "config": {
+                "workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x {nsub} "
+                            f"sub-bands x {L} bins): dedispersion, 0..255 profile, 100-DM "
+                            f"chi^2 curve, 8 Lyon features (pfe_pfd_dmprof)",
+                "candidates_per_gpu": n,
+                "fold_shape": list(pfd_shape),
+                "parallelism": f"candidate shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "pfe::k_pfd_dmprof",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "avg_kernel_ms": kern_ms,
+                "avg_kernel_ms_max_over_ranks": kern_ms_max,
+            },
+        }
     else:
         ops = load_ops_per_candidate()
         achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
@@ -300,6 +393,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         if args.path == "lyon8":
             result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
+        elif args.path == "pfd":
+            result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
         else:
             result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
     if rank == 0:
