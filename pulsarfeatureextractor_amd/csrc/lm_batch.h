@@ -154,21 +154,9 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
 #pragma unroll
   for (int j = 0; j < N; ++j)
     if (lane <= j) S.r[tri_idx(0, j) + lane][f] = fjac[0][j];
-  // scaled gradient norm
-  double gnorm = 0.0;
-  if (fnorm != 0.0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const double wl = sel(acn, ipvt[j]);
-      if (wl != 0.0) {
-        double sum = 0.0;
-#pragma unroll
-        for (int i = 0; i <= j; ++i) sum += bcast(fjac[0][j], i) * (qtf[i] / fnorm);
-        gnorm = fmax(gnorm, fabs(sum / wl));
-      }
-    }
-  }
-  const int info = (gnorm <= LM_GTOL) ? 4 : 0;
+  // the scaled gradient norm and the gtol test run in the next SIMT phase (blm_simt), one
+  // fit per lane, from R, qtf, acnorm and ipvt in LDS; info = -1 marks "not yet tested"
+  const int info = -1;
   if (lane == 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -177,7 +165,6 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
       S.acn[j][f] = acn[j];
       S.ipvt[j][f] = ipvt[j];
     }
-    S.gnorm[f] = gnorm;
     S.info[f] = info;
     S.nfev[f] = nfev;
     S.iter[f] = iter;
@@ -219,6 +206,29 @@ __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
   double delta = S.delta[f], par = S.par[f];
   const double fnorm = S.fnorm[f];
   const int iter = S.iter[f];
+  if (S.info[f] < 0) {
+    // scaled gradient norm of the new Jacobian and the gtol test (lmdif's outer loop)
+    double acn[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) acn[j] = S.acn[j][f];
+    double gnorm = 0.0;
+    if (fnorm != 0.0) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const double wl = sel(acn, ipvt[j]);
+        if (wl != 0.0) {
+          double sum = 0.0;
+#pragma unroll
+          for (int i = 0; i <= j; ++i) sum += r[i][j] * (qtf[i] / fnorm);
+          gnorm = fmax(gnorm, fabs(sum / wl));
+        }
+      }
+    }
+    S.gnorm[f] = gnorm;
+    const int info = (gnorm <= LM_GTOL) ? 4 : 0;
+    S.info[f] = info;
+    if (info != 0) return;
+  }
   double wa1[N], wa2[N], wa3[N];
   lmpar<N>(r, ipvt, diag, qtf, delta, par, wa1, wa2);
 #pragma unroll
@@ -342,11 +352,12 @@ __device__ __forceinline__ void blm_run(const Loader& load, BlmState<N, FPW>& S,
   }
   for (;;) {
     blm_sync();
-    const bool mine = lane < FPW && ((fits >> lane) & 1ull) && S.info[lane < FPW ? lane : 0] == 0;
-    const uint64_t act = __ballot(mine);
-    if (act == 0) break;
+    const bool mine = lane < FPW && ((fits >> lane) & 1ull) && S.info[lane < FPW ? lane : 0] <= 0;
+    if (__ballot(mine) == 0) break;
     if (mine) blm_simt<N, FPW>(lane, S);
     blm_sync();
+    // fits still iterating after the gtol test: evaluate their trial points
+    const uint64_t act = __ballot(mine && S.info[lane < FPW ? lane : 0] == 0);
     for (uint64_t m = act; m; m &= m - 1) {
       const int f = __builtin_ctzll(m);
       const auto fn = load(f);
