@@ -15,16 +15,30 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st);
 hipError_t launch_subband(const BatesArgs& a, hipStream_t st);
 
-// persistent waves of the batched kernels: enough to fill every CU (8 waves each), never
-// more than there are batches
-static int persistent_waves(int64_t n) {
+static int device_cus() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
       cus = v;
   }
-  const int64_t batches = (n + BLM_FPW - 1) / BLM_FPW;
+  return cus;
+}
+
+// Fits per wave of the batched kernels: as many as fit the LDS state (32), but few enough
+// that the grid holds ~4 waves for every one of (CUs x 16) wave slots -- each wave runs its
+// fits one after another, so a batch of fewer waves than slots finishes with its slowest wave
+static int blm_fits_per_wave(int64_t n, int cus) {
+  const int64_t f = n / ((int64_t)cus * 64);
+  return (int)(f < 4 ? 4 : f > BLM_FPW ? BLM_FPW : f);
+}
+
+// persistent waves of the batched kernels: enough to fill every CU (8 waves each), never
+// more than there are batches
+static int persistent_waves(int64_t n) {
+  const int cus = device_cus();
+  const int fpw = blm_fits_per_wave(n, cus);
+  const int64_t batches = (n + fpw - 1) / fpw;
   const int64_t w = (int64_t)cus * 8;
   return (int)(batches < w ? (batches > 0 ? batches : 1) : w);
 }
@@ -65,6 +79,7 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(in->n);
+  a.fpw = blm_fits_per_wave(in->n, device_cus());
   // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code
   a.c_lp = std::pow((double)in->lp, -0.3333333);
   a.c_lp1 = std::pow((double)(in->lp - 1), -0.3333333);

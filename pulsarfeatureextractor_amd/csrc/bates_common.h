@@ -46,11 +46,13 @@ struct BatesArgs {
   unsigned* counters;  // BATES_NCOUNTERS work-queue counters, zeroed before the chain
   double* wscr;        // per-wave scratch of the persistent batched kernels
   int pwaves;          // number of persistent waves wscr is sized for
+  int fpw;             // fits per wave of the batched kernels (<= BLM_FPW): small batches
+                       // use fewer so that there are several waves per wave slot
 };
 
 constexpr int BATES_NCOUNTERS = 16;
 constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
-constexpr int BLM_FPW = 32;  // fits per wave in the batched kernels
+constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS state size)
 
 // rows per lane (MPL) the kernels use for a profile of lp bins
 __host__ __device__ constexpr int profile_mpl(int lp) {

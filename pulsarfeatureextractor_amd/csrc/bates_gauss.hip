@@ -371,37 +371,56 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
 // ---------------------------------------------------------------------------------------
 template <int MPL>
 struct GaussBgFn {  // y - (|A| exp(-((x-mu)/|sigma|)^2/2) + bg)      (:1226)
+  static constexpr bool kCols = true;  // amplitude / background columns reuse the exp
+  struct Cache {
+    double e[MPL];
+  };
   double x[MPL], y[MPL];
   bool ok[MPL];
-  __device__ __forceinline__ double model(const double (&p)[4], int k) const {
+  __device__ __forceinline__ double term(const double (&p)[4], int k) const {
     const double t = (x[k] - p[1]) / fabs(p[0]);
-    return fabs(p[2]) * exp(-(t * t) / 2.0) + p[3];
+    return exp(-(t * t) / 2.0);
+  }
+  __device__ __forceinline__ double model(const double (&p)[4], int k) const {
+    return fabs(p[2]) * term(p, k) + p[3];
   }
   __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
   }
+  __device__ __forceinline__ void eval(const double (&p)[4], double (&f)[MPL], Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      c.e[k] = ok[k] ? term(p, k) : 0.0;
+      f[k] = ok[k] ? y[k] - (fabs(p[2]) * c.e[k] + p[3]) : 0.0;
+    }
+  }
+  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double (&f)[MPL],
+                                           const Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      const double e = (j < 2) ? (ok[k] ? term(p, k) : 0.0) : c.e[k];
+      f[k] = ok[k] ? y[k] - (fabs(p[2]) * e + p[3]) : 0.0;
+    }
+  }
 };
 
+// fitGaussianT1's data (:1097-1132): the halves-rotated, background-shifted profile, and the
+// start point of fitGaussianWithBackground (:1239-1245)
 template <int P>
-__global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+__device__ __forceinline__ void gt1_setup(const BatesArgs& a, int64_t c, const GaussWS& w,
+                                          GaussBgFn<P>& fn) {
   const int lane = lane_id();
   const int lp = a.lp;
   const int cut = lp / 2;  // Py2: ceil(L/2) of an int division is L//2
-  const GaussWS w = a.ws[c];
-  GaussBgFn<P> fn;
-  bool ok[P];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int i = lane + 64 * k;
-    ok[k] = i < lp;
-    fn.ok[k] = ok[k];
+    const bool ok = i < lp;
+    fn.ok[k] = ok;
     fn.x[k] = (double)i;
     double y = 0.0;
-    if (ok[k]) {
+    if (ok) {
       const int src = (i + cut) % lp;  // rotated: part2 + part1 (:1107-1109)
       const double pv = (double)a.prof[c * lp + src];
       if (w.minbg > 0.0) {
@@ -413,27 +432,42 @@ __global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
     }
     fn.y[k] = y;
   }
-  // initial parameters (:1239-1245)
+}
+
+template <int P>
+__device__ __forceinline__ void gt1_start(const GaussBgFn<P>& fn, int lp, double (&p)[4]) {
+  const int lane = lane_id();
   double bv = -INFINITY;
   int bi = 1 << 30;
 #pragma unroll
   for (int k = 0; k < P; ++k)
-    if (ok[k] && (bi == (1 << 30) || fn.y[k] > bv)) {
+    if (fn.ok[k] && (bi == (1 << 30) || fn.y[k] > bv)) {
       bv = fn.y[k];
       bi = lane + 64 * k;
     }
   const ArgMax am = wargmax(bv, bi);
+  bool ok[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) ok[k] = fn.ok[k];
   const FMeanStd fs = f_mean_std<P>(fn.y, ok, lp);
-  double p[4] = {fs.std, (double)am.i, am.v, 1.0};
-  lmdif<4, P>(fn, p, 200 * 5);
+  p[0] = fs.std;
+  p[1] = (double)am.i;
+  p[2] = am.v;
+  p[3] = 1.0;
+}
+
+template <int P>
+__device__ __forceinline__ void gt1_finish(const BatesArgs& a, int64_t c, const GaussBgFn<P>& fn,
+                                           const double (&p)[4]) {
+  const int lane = lane_id();
   double cs = 0.0;
 #pragma unroll
   for (int k = 0; k < P; ++k)
-    if (ok[k]) {
+    if (fn.ok[k]) {
       const double dd = fn.y[k] - fn.model(p, k);
       cs += dd * dd;
     }
-  const double chisq = wsum(cs) / (double)lp;
+  const double chisq = wsum(cs) / (double)a.lp;
   if (lane == 0) {
     double* o = a.out + c * 22;
     o[7] = fabs(FWHM_C * p[0]);  // s8 (:1247)
@@ -443,6 +477,63 @@ __global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
     wp->t1[1] = p[1];
     wp->t1[2] = p[2];
     wp->t1[3] = p[3];
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  const GaussWS w = a.ws[c];
+  GaussBgFn<P> fn;
+  gt1_setup<P>(a, c, w, fn);
+  double p[4];
+  gt1_start<P>(fn, a.lp, p);
+  lmdif<4, P>(fn, p, 200 * 5);
+  gt1_finish<P>(a, c, fn, p);
+}
+
+// batched form (lm_batch.h); bit-identical to k_gt1
+template <int P>
+struct Gt1Loader {
+  BatesArgs a;
+  int64_t base;
+  __device__ __forceinline__ GaussBgFn<P> operator()(int f) const {
+    GaussBgFn<P> fn;
+    gt1_setup<P>(a, base + f, a.ws[base + f], fn);
+    return fn;
+  }
+};
+
+template <int P>
+__global__ __launch_bounds__(64) void k_gt1b(BatesArgs a) {
+  constexpr int FPW = BLM_FPW;
+  __shared__ BlmState<4, FPW> S;
+  const int fpw = a.fpw;
+  const int64_t base = (int64_t)blockIdx.x * fpw;
+  const int lane = lane_id();
+  const bool live = lane < fpw && base + lane < a.n &&
+                    !(a.status[base + (lane < fpw ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
+  const uint64_t fits = __ballot(live);
+  if (fits == 0) return;
+  const Gt1Loader<P> load{a, base};
+  for (uint64_t m = fits; m; m &= m - 1) {
+    const int f = __builtin_ctzll(m);
+    const GaussBgFn<P> fn = load(f);
+    double p[4];
+    gt1_start<P>(fn, a.lp, p);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) S.x[j][f] = p[j];
+    }
+  }
+  blm_run<4, P, FPW>(load, S, fits, 200 * 5);
+  for (uint64_t m = fits; m; m &= m - 1) {
+    const int f = __builtin_ctzll(m);
+    const GaussBgFn<P> fn = load(f);
+    const double p[4] = {S.x[0][f], S.x[1][f], S.x[2][f], S.x[3][f]};
+    gt1_finish<P>(a, base + f, fn, p);
   }
 }
 
@@ -848,16 +939,17 @@ __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
   double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(L);
   double* yv = xs + (size_t)FPW * 64 * P;
   const PeelLoader<P> load{xs, yv, mpad};
-  const int64_t nb = (a.n + FPW - 1) / FPW;
+  const int fpw = a.fpw;
+  const int64_t nb = (a.n + fpw - 1) / fpw;
   for (;;) {
     int b = 0;
     if (lane == 0) b = (int)atomicAdd(a.counters + CTR_GDG, 1u);
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= nb) break;
-    const int64_t base = (int64_t)b * FPW;
+    const int64_t base = (int64_t)b * fpw;
     // candidates of this batch that reach the double-Gaussian fit
-    const bool live = lane < FPW && base + lane < a.n &&
-                      !(a.status[base + (lane < FPW ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
+    const bool live = lane < fpw && base + lane < a.n &&
+                      !(a.status[base + (lane < fpw ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
     uint64_t fits = __ballot(live);
     // prologue: peak removal, pass-1 rows and start points
     for (uint64_t m = fits; m; m &= m - 1) {
@@ -1048,10 +1140,10 @@ struct Gdg8Loader {
 template <int P, int FPW>
 __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
   __shared__ BlmState<8, FPW> S;
-  const int64_t base = (int64_t)blockIdx.x * FPW;
+  const int64_t base = (int64_t)blockIdx.x * a.fpw;
   const int lane = lane_id();
   bool part = false;
-  if (lane < FPW) {
+  if (lane < a.fpw) {
     const int64_t c = base + lane;
     if (c < a.n && !(a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR))) {
       part = true;
@@ -1092,13 +1184,17 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   do {                                                                                  \
     hipLaunchKernelGGL((k_ghist<P, 4, false>), gw(a.n), dim3(BLOCK), 0, st, a);         \
     hipLaunchKernelGGL((k_ghist<P, 16, true>), gw(a.n), dim3(BLOCK), 0, st, a);         \
-    hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                     \
+    if (use_blm)                                                                        \
+      hipLaunchKernelGGL((k_gt1b<P>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)),      \
+                         dim3(64), 0, st, a);                                           \
+    else                                                                                \
+      hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
     if (use_blm)                                                                        \
       hipLaunchKernelGGL((k_gdgb<P>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);    \
     else                                                                                \
       hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
     if (use_blm)                                                                        \
-      hipLaunchKernelGGL((k_gdg8b<P, BLM_FPW>), dim3((unsigned)((a.n + BLM_FPW - 1) / BLM_FPW)), \
+      hipLaunchKernelGGL((k_gdg8b<P, BLM_FPW>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)), \
                          dim3(64), 0, st, a);                                           \
     else                                                                                \
       hipLaunchKernelGGL((k_gdg8<P>), gw(a.n), dim3(BLOCK), 0, st, a);                  \

@@ -10,6 +10,7 @@
 //   s20-s22 PHCXOperations.getSubbandParameters :305-349, getProfileCorr :387-415,
 //           ProfileOperations.getSubband_scores :1585-1686
 #include "bates_common.h"
+#include "lm_batch.h"
 
 namespace pfe {
 
@@ -165,17 +166,39 @@ constexpr double F3 = 2593941624.0;       // pow(1374, 3), an exact integer
 
 template <int MPL>
 struct DMFn {
+  static constexpr bool kCols = true;  // the amplitude column reuses sqrt((P - w)/w)
+  struct Cache {
+    double s[MPL];
+  };
   double x[MPL], y[MPL];
   bool ok[MPL];
   double wint, dm, period;
-  __device__ __forceinline__ double model(const double (&p)[3], int k) const {
+  __device__ __forceinline__ double shape(const double (&p)[3], int k) const {
     const double t = p[1] * KDM * fabs((dm + p[2]) - x[k]) * DF / F3;   // :152
     const double weff = sqrt(wint + t * t);
-    return p[0] * sqrt((period - weff) / weff);                        // :153
+    return sqrt((period - weff) / weff);
+  }
+  __device__ __forceinline__ double model(const double (&p)[3], int k) const {
+    return p[0] * shape(p, k);                                         // :153
   }
   __device__ __forceinline__ void operator()(const double (&p)[3], double (&f)[MPL]) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - model(p, k) : 0.0;
+  }
+  __device__ __forceinline__ void eval(const double (&p)[3], double (&f)[MPL], Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      c.s[k] = ok[k] ? shape(p, k) : 0.0;
+      f[k] = ok[k] ? y[k] - p[0] * c.s[k] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void eval_col(const double (&p)[3], int j, double (&f)[MPL],
+                                           const Cache& c) const {
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      const double sh = (j == 0) ? c.s[k] : (ok[k] ? shape(p, k) : 0.0);
+      f[k] = ok[k] ? y[k] - p[0] * sh : 0.0;
+    }
   }
 };
 
@@ -184,53 +207,75 @@ __device__ __forceinline__ double filter_neg(double v) {
   return (fabs(v - 0.0) > 0.000005 && v < 0.0) ? 0.0 : v;
 }
 
+// the DM-curve fit data of candidate c (:160-209): residual functor, theoretical curve
+// shape help[] and the start amplitude 255/max(help)
 template <int MPL>
-__global__ __launch_bounds__(BLOCK) void k_dmfit(BatesArgs a) {
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
+struct DMSetup {
+  DMFn<MPL> fn;
+  double help[MPL];
+  double amp0;
+};
+
+// the residual functor alone (what an m-phase visit of the batched solver rebuilds)
+template <int MPL>
+__device__ __forceinline__ void dm_functor(const BatesArgs& a, int64_t c, DMFn<MPL>& fn) {
   const int lane = lane_id();
   const double* sc = a.scal + c * PFE_NSCAL;
-  const double period = sc[PFE_SCAL_PERIOD_MS], snr = sc[PFE_SCAL_SNR], dm = sc[PFE_SCAL_DM],
+  const double period = sc[PFE_SCAL_PERIOD_MS], dm = sc[PFE_SCAL_DM],
                width = sc[PFE_SCAL_WIDTH], dm_start = sc[PFE_SCAL_DM_START],
                dm_end = sc[PFE_SCAL_DM_END], length_all = sc[PFE_SCAL_LENGTH_ALL];
   const int n = a.ndm;
-  DMFn<MPL> fn;
   const double step = fabs(dm_start - dm_end) / length_all;          // :183
-  const double wint = (width * period) * (width * period);           // :186
-  fn.wint = wint;
+  fn.wint = (width * period) * (width * period);                     // :186
   fn.dm = dm;
   fn.period = period;
-  double help[MPL];
-  double hmax = -INFINITY;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) {
     const int i = lane + 64 * k;
     fn.ok[k] = i < n;
-    fn.y[k] = fn.ok[k] ? a.dmcurve[c * n + i] : 0.0;
+    fn.y[k] = fn.ok[k] ? a.dmcurve[c * n + (fn.ok[k] ? i : 0)] : 0.0;
     fn.x[k] = dm_start + (double)(128 * i - 1) * step;               // :196 (x = 128k-1)
-    const double t = KDM * fabs(dm - fn.x[k]) * DF / F3;
+  }
+}
+
+template <int MPL>
+__device__ __forceinline__ void dm_setup(const BatesArgs& a, int64_t c, DMSetup<MPL>& d) {
+  dm_functor<MPL>(a, c, d.fn);
+  const double wint = d.fn.wint, dm = d.fn.dm, period = d.fn.period;
+  double hmax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const double t = KDM * fabs(dm - d.fn.x[k]) * DF / F3;
     const double weff = sqrt(wint + t * t);                          // :202
-    help[k] = sqrt((period - weff) / weff);                          // :203
-    if (fn.ok[k]) hmax = fmax(hmax, help[k]);
+    d.help[k] = sqrt((period - weff) / weff);                        // :203
+    if (d.fn.ok[k]) hmax = fmax(hmax, d.help[k]);
   }
   hmax = wmax(hmax);
   // Python max(): a leading NaN wins, later NaNs are skipped
-  const double h0 = bcast(help[0], 0);
+  const double h0 = bcast(d.help[0], 0);
   if (h0 != h0) hmax = h0;
-  const double amp0 = 255.0 / hmax;                                  // :206-209
-  double p[3] = {amp0, 1.0, 0.0};
-  lmdif<3, MPL>(fn, p, 200 * 4);
+  d.amp0 = 255.0 / hmax;                                             // :206-209
+}
+
+template <int MPL>
+__device__ __forceinline__ void dm_finish(const BatesArgs& a, int64_t c, const DMSetup<MPL>& d,
+                                          const double (&p)[3]) {
+  const int lane = lane_id();
+  const double* sc = a.scal + c * PFE_NSCAL;
+  const double period = sc[PFE_SCAL_PERIOD_MS], snr = sc[PFE_SCAL_SNR], dm = sc[PFE_SCAL_DM],
+               width = sc[PFE_SCAL_WIDTH];
+  const double wint = d.fn.wint;
   double chi = 0.0;
 #pragma unroll
   for (int k = 0; k < MPL; ++k)
-    if (fn.ok[k]) {
-      const double fit = fn.model(p, k);
+    if (d.fn.ok[k]) {
+      const double fit = d.fn.model(p, k);
       if (fit >= 1.0) {
-        const double d = fn.y[k] - amp0 * help[k];                   // theo (:206)
-        chi += d * d;
+        const double dd = d.fn.y[k] - d.amp0 * d.help[k];            // theo (:206)
+        chi += dd * dd;
       }
     }
-  chi = wsum(chi) / (double)n;                                       // :222-229
+  chi = wsum(chi) / (double)a.ndm;                                   // :222-229
   if (lane == 0) {
     double* o = a.out + c * 22;
     o[11] = period;                                                  // s12
@@ -241,6 +286,59 @@ __global__ __launch_bounds__(BLOCK) void k_dmfit(BatesArgs a) {
     o[16] = fabs(1.0 - p[1]);                                        // s17
     o[17] = fabs(p[2]);                                              // s18 (filterScore 18)
     o[18] = chi;                                                     // s19
+  }
+}
+
+template <int MPL>
+__global__ __launch_bounds__(BLOCK) void k_dmfit(BatesArgs a) {
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  DMSetup<MPL> d;
+  dm_setup<MPL>(a, c, d);
+  double p[3] = {d.amp0, 1.0, 0.0};
+  lmdif<3, MPL>(d.fn, p, 200 * 4);
+  dm_finish<MPL>(a, c, d, p);
+}
+
+// batched form: one wave owns BLM_FPW candidates' DM fits (lm_batch.h); bit-identical
+template <int MPL>
+struct DMLoader {
+  BatesArgs a;
+  int64_t base;
+  __device__ __forceinline__ DMFn<MPL> operator()(int f) const {
+    DMFn<MPL> fn;
+    dm_functor<MPL>(a, base + f, fn);
+    return fn;
+  }
+};
+
+template <int MPL>
+__global__ __launch_bounds__(64) void k_dmfitb(BatesArgs a) {
+  constexpr int FPW = BLM_FPW;
+  __shared__ BlmState<3, FPW> S;
+  const int64_t base = (int64_t)blockIdx.x * a.fpw;
+  const int lane = lane_id();
+  const bool live = lane < a.fpw && base + lane < a.n;
+  const uint64_t fits = __ballot(live);
+  if (fits == 0) return;
+  for (uint64_t m = fits; m; m &= m - 1) {
+    const int f = __builtin_ctzll(m);
+    DMSetup<MPL> d;
+    dm_setup<MPL>(a, base + f, d);
+    if (lane == 0) {
+      S.x[0][f] = d.amp0;
+      S.x[1][f] = 1.0;
+      S.x[2][f] = 0.0;
+    }
+  }
+  const DMLoader<MPL> load{a, base};
+  blm_run<3, MPL, FPW>(load, S, fits, 200 * 4);
+  for (uint64_t m = fits; m; m &= m - 1) {
+    const int f = __builtin_ctzll(m);
+    DMSetup<MPL> d;
+    dm_setup<MPL>(a, base + f, d);
+    const double p[3] = {S.x[0][f], S.x[1][f], S.x[2][f]};
+    dm_finish<MPL>(a, base + f, d, p);
   }
 }
 
@@ -683,6 +781,19 @@ hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
+  const char* blm_env = getenv("PFE_BLM");
+  if (!(blm_env && blm_env[0] == '0')) {  // batched lmdif (lm_batch.h)
+    const dim3 g((unsigned)((a.n + a.fpw - 1) / a.fpw));
+    if (a.ndm <= 64)
+      hipLaunchKernelGGL(k_dmfitb<1>, g, dim3(64), 0, st, a);
+    else if (a.ndm <= 128)
+      hipLaunchKernelGGL(k_dmfitb<2>, g, dim3(64), 0, st, a);
+    else if (a.ndm <= 256)
+      hipLaunchKernelGGL(k_dmfitb<4>, g, dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_dmfitb<16>, g, dim3(64), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.ndm <= 64)
     hipLaunchKernelGGL(k_dmfit<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else if (a.ndm <= 128)
