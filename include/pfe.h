@@ -164,6 +164,7 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
 #define PFE_PFD_DM_LO 4
 #define PFE_PFD_DM_HI 5
 #define PFE_PFD_NUMDMS 6
+#define PFE_PFD_BARY_P1 7 /* bary_p1 (s; the 22-score path: period = bary_p1 * 1000) */
 #define PFE_PFD_NDM 100
 #define PFE_ST_PFD_DMCURVE_FAIL 0x020u
 
@@ -177,6 +178,16 @@ typedef struct pfe_pfd_in {
 
 int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* chis,
                    double* lyon8, uint32_t* status, uint32_t flags);
+
+/* pfe_pfd_bates22 <- PFDFile.compute (PFDFile.py:587-613): the 22 scores of each fold in the
+ * reference's order -- ProfileOperations' sinusoid and Gaussian fits on the 0..255 float
+ * profile (s1-s11), PFDOperations.getCandidateParameters (s12-s15, PFDOperations.py:93-233),
+ * getDMFittings (s16-s19, the clamped 4-parameter fit to the chi^2-vs-DM curve, :274-393) and
+ * getSubbandParameters over the dedispersed sub-band profiles (s20-s22, :401-466).
+ * Same inputs as pfe_pfd_dmprof (scal[PFE_PFD_BARY_P1] is used); out[n][22]; status bits as
+ * pfe_bates22 (PFE_ST_DMFIT_FAIL when numdms == 1).  LDS-resident limit as pfe_pfd_dmprof. */
+int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* status,
+                    uint32_t flags);
 
 #ifdef __cplusplus
 }

@@ -119,8 +119,10 @@ def fit_sine(y, maxima):
         phi0 = 0
     elif y[0] < bg:
         phi0 = -1 / (4 * f0) if f0 != 0 else -1.0 / (4.0 * 0.00000000001)
-    else:
+    elif y[0] > bg:
         phi0 = +1 / (4 * f0) if f0 != 0 else +1.0 / (4.0 * 0.00000000001)
+    else:  # NaN (a float PFD profile of a constant fold): phi0 never assigned (:427-441)
+        raise UnboundLocalError("local variable 'phi0' referenced before assignment")
     p = leastsq(lambda p_, x_, y_: y_ - model(p_, x_), (f0, phi0), args=(x, y), full_output=True)[0]
     return _chisq_mean(y, model(p, x))
 
@@ -452,15 +454,14 @@ def subband_scores(sub, profile, width):
             row.append(s)
         sums.append(row)
     max_bins = []
-    for i in range(len(sums)):
+    mb = None  # max_bin is one local across the bands: a band with no sum > -10000 repeats
+    for i in range(len(sums)):  # the previous band's position (:1619-1628)
         best = -10000.0
-        have = False
         for j in range(len(sums[i])):
             if sums[i][j] > best:
                 best = sums[i][j]
                 mb = j + wb // 2
-                have = True
-        if not have:
+        if mb is None:
             raise UnboundLocalError("max_bin referenced before assignment")
         max_bins.append(float(mb))
     med = np.array(max_bins).mean()

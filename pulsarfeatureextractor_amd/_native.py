@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "pfe_lyon8_f64",
     "pfe_bates22",
     "pfe_pfd_dmprof",
+    "pfe_pfd_bates22",
 )
 PFE_PFD_NSCAL = 8
 PFE_PFD_NDM = 100
@@ -164,6 +165,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
         lib.pfe_pfd_dmprof.restype = C.c_int
         lib.pfe_pfd_dmprof.argtypes = [vp, C.POINTER(PfdIn), vp, vp, vp, vp, u32]
+        lib.pfe_pfd_bates22.restype = C.c_int
+        lib.pfe_pfd_bates22.argtypes = [vp, C.POINTER(PfdIn), vp, vp, u32]
         pp = C.POINTER(C.c_char_p)
         lib.pfe_phcx_parse.restype = C.c_int
         lib.pfe_phcx_parse.argtypes = [pp, i64, i32, i32, C.POINTER(vp)]
@@ -369,6 +372,35 @@ class Engine:
             _ptr(out["chis"]) if chis else None, _ptr(out["lyon8"]) if lyon8 else None,
             _ptr(out["status"]), flags))
         return out
+
+
+    def pfd_bates22(self, profs, subfreqs, scal):
+        """The 22 scores of PFD folds (pfe_pfd_bates22, PFDFile.compute) for a batch of one
+        shape: profs (n,npart,nsub,L) f64, subfreqs (n,nsub), scal (n,PFE_PFD_NSCAL) with
+        scal[:, 7] = bary_p1.  Returns (out (n,22) f64, status (n,))."""
+        n, npart, nsub, L = profs.shape
+        if subfreqs.shape != (n, nsub) or scal.shape != (n, PFE_PFD_NSCAL):
+            raise ValueError("pfd_bates22: subfreqs must be (n,nsub), scal (n,%d)" % PFE_PFD_NSCAL)
+        if _is_device(profs):
+            import torch
+
+            self._follow_torch()
+            for t in (profs, subfreqs, scal):
+                if not t.is_contiguous():
+                    raise ValueError("pfd_bates22: device tensors must be contiguous")
+            out = torch.empty((n, 22), dtype=torch.float64, device=profs.device)
+            status = torch.empty((n,), dtype=torch.int32, device=profs.device)
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            profs = np.ascontiguousarray(profs, dtype=np.float64)
+            subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
+            scal = np.ascontiguousarray(scal, dtype=np.float64)
+            out = np.empty((n, 22), dtype=np.float64)
+            status = np.empty((n,), dtype=np.uint32)
+            flags = 0
+        pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
+        self._check(self.lib.pfe_pfd_bates22(self._h, C.byref(pin), _ptr(out), _ptr(status), flags))
+        return out, status
 
 
 class PhcxBatch:

@@ -18,6 +18,7 @@ import threading
 
 import numpy as np
 
+from . import pfd as _pfd
 from . import phcx as _phcx
 from ._native import (PFE_ST_DMFIT_FAIL, PFE_ST_GAUSS_FAIL, PFE_ST_SINE_FAIL,
                       PFE_ST_SUBBAND_FAIL, Engine)
@@ -172,6 +173,63 @@ class SUPERBPHCXFile(PHCXFile):
     SUPERB = True
 
 
+class PFDFile(CandidateFileInterface):
+    """PFDFile.PFD (PFDFile.py:64-875): a PRESTO fold read on the host (pfd.read, :96-252),
+    scored through pfe_pfd_bates22 / pfe_pfd_dmprof."""
+
+    def __init__(self, debugFlag, candidateName, engine=None):
+        super().__init__(debugFlag)
+        self.cand = candidateName
+        self.engine = engine or get_engine()
+        self.data = _pfd.read(candidateName)
+        self.scores = []
+
+    def _batch(self):
+        return _pfd.batch_inputs([self.data])
+
+    def _dmprof(self):
+        profs, subfreqs, scal = self._batch()
+        return self.engine.pfd_dmprof(profs, subfreqs, scal)
+
+    def isValid(self):
+        return self.data.proflen > 0 and self.data.numchan > 0          # :460-475
+
+    def getProfile(self):
+        return self._dmprof()["profile"][0]
+
+    def compute(self):
+        """PFDFile.compute (:587-613): the 22 scores."""
+        out, st = self.engine.pfd_bates22(*self._batch())
+        msg = status_error(int(st[0]))
+        if msg:
+            raise Exception(msg)
+        self.scores = [float(v) for v in out[0]]
+        return self.scores
+
+    def computeProfileScores(self):
+        """:479-492 — the 0..255 profile bins."""
+        self.scores = [float(v) for v in self.getProfile()]
+        return self.scores
+
+    def computeProfileStatScores(self):
+        """:522-551"""
+        return [float(v) for v in self._dmprof()["lyon8"][0, :4]]
+
+    def computeDMCurveStatScores(self):
+        """:553-583"""
+        r = self._dmprof()
+        if int(r["status"][0]) & 0x20:
+            raise Exception("DM curve stat score extraction exception")
+        return [float(v) for v in r["lyon8"][0, 4:]]
+
+    def getDMCurveData(self):
+        """:494-520 — the float32 chi^2-vs-DM curve."""
+        r = self._dmprof()
+        if int(r["status"][0]) & 0x20:
+            raise Exception("DM curve extraction exception")
+        return r["chis"][0]
+
+
 class Candidate:
     """Candidate.py:42-547 with the same methods and file-name dispatch (:136-150)."""
 
@@ -185,8 +243,7 @@ class Candidate:
 
     def _file(self, verbose):
         if ".pfd" in self.candidateName:
-            raise NotImplementedError("PFD candidates are not supported by this build "
-                                      "(SURVEY.md §8(f) 'next' row)")
+            return PFDFile(verbose, self.candidateName)
         if ".gz" in self.candidateName:
             return PHCXFile(verbose, self.candidateName)
         return SUPERBPHCXFile(verbose, self.candidateName)

@@ -3,9 +3,9 @@
   python -m pulsarfeatureextractor_amd.cli -c <dir|file> -o <out> [--phcx|--superb]
          [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K]
 
-Same flags, same output-file probing (:147-160), same mode dispatch (:215-290).  PFD files
-are served in --dmprof and --profile modes; the PFD 22-score modes and --label (interactive
-labelling) are recognised and refused with exit status 2.
+Same flags, same output-file probing (:147-160), same mode dispatch (:215-290), for PHCX,
+SUPERB and PFD files in every mode.  --label (interactive labelling) is recognised and refused
+with exit status 2.
 """
 from __future__ import annotations
 

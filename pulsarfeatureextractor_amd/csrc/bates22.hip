@@ -57,11 +57,36 @@ __global__ void k_clear_internal(uint32_t* status, int64_t n) {
   if (i < n) status[i] &= 0xFFFFu;
 }
 
+void launch_clear_internal(uint32_t* status, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_clear_internal, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     status, n);
+}
+
+// workspace pointers, batching parameters and the Freedman-Diaconis constants of a chain
+// over n candidates of lp bins (work: bates22_workspace_bytes)
+void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
+  char* wb = (char*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
+  a.ws = (GaussWS*)wb;
+  wb += align256((size_t)n * sizeof(GaussWS));
+  a.counters = (unsigned*)wb;
+  wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
+  a.wscr = (double*)wb;
+  a.pwaves = persistent_waves(n);
+  a.fpw = blm_fits_per_wave(n, device_cus());
+  a.lp = lp;
+  a.n = n;
+  // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code
+  a.c_lp = std::pow((double)lp, -0.3333333);
+  a.c_lp1 = std::pow((double)(lp - 1), -0.3333333);
+}
+
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
                           size_t work_bytes, hipStream_t st) {
   if (work_bytes < bates22_workspace_bytes(in)) return hipErrorInvalidValue;
   BatesArgs a;
+  bates_setup(a, in->n, in->lp, work);
   a.prof = in->prof;
+  a.fprof = nullptr;
   a.lp = in->lp;
   a.sub = in->sub;
   a.nsub = in->nsub;
@@ -72,17 +97,6 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   a.n = in->n;
   a.out = out;
   a.status = status;
-  char* wb = (char*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
-  a.ws = (GaussWS*)wb;
-  wb += align256((size_t)in->n * sizeof(GaussWS));
-  a.counters = (unsigned*)wb;
-  wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
-  a.wscr = (double*)wb;
-  a.pwaves = persistent_waves(in->n);
-  a.fpw = blm_fits_per_wave(in->n, device_cus());
-  // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code
-  a.c_lp = std::pow((double)in->lp, -0.3333333);
-  a.c_lp1 = std::pow((double)(in->lp - 1), -0.3333333);
   hipError_t e = hipMemsetAsync(status, 0, (size_t)in->n * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(out, 0, (size_t)in->n * 22 * sizeof(double), st);
@@ -93,8 +107,7 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   if ((e = launch_gauss(a, st)) != hipSuccess) return e;
   if ((e = launch_dmfit(a, st)) != hipSuccess) return e;
   if ((e = launch_subband(a, st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_clear_internal, dim3((unsigned)((in->n + 255) / 256)), dim3(256), 0, st,
-                     status, in->n);
+  launch_clear_internal(status, in->n, st);
   return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@ struct GaussWS {
 
 struct BatesArgs {
   const uint8_t* prof;
+  const double* fprof;  // float profiles (the PFD path, pfd22.hip) instead of prof, or null
   int lp;
   const uint8_t* sub;
   int nsub, lsb;
@@ -69,6 +70,12 @@ static inline dim3 grid_for_candidates(int64_t n) {
 
 __device__ __forceinline__ int64_t wave_candidate() {
   return ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+}
+
+// one profile value as fp64: the uint8 PHCX row, or the float PFD row when fprof is set
+// (a uniform branch on a kernel argument)
+__device__ __forceinline__ double prof_at(const BatesArgs& a, int64_t idx) {
+  return a.fprof ? a.fprof[idx] : (double)a.prof[idx];
 }
 
 // Profile row of candidate c into MPL slots (rows beyond lp read 0).

@@ -14,7 +14,10 @@
 //   k_gdg    : peak peeling, 8 single-Gaussian passes with subtraction, the 8-parameter
 //              fit and the combination rule -> s10, s11
 #include "bates_common.h"
+#include <type_traits>
+
 #include "lm_batch.h"
+#include "np_sum.h"
 
 namespace pfe {
 
@@ -65,17 +68,86 @@ __device__ int fd_bins(const int (&v)[MPL], const bool (&ok)[MPL], int n, double
   return q > 1e9 ? 1000000000 : (int)q;
 }
 
-// numpy.histogram(data, nbins) of integers into per-wave LDS counters
+// ---- the same for float data (PFD profiles) ----
+// doubles ordered as unsigned keys (finite data)
+__device__ __forceinline__ uint64_t okey(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double from_okey(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// k-th smallest (0-based) value of v[ok] by bisection over the key range (64 ballots rounds)
+template <int MPL>
+__device__ double kth_smallest_f(const double (&v)[MPL], const bool (&ok)[MPL], int k) {
+  uint64_t kv[MPL];
+  uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+  for (int s = 0; s < MPL; ++s) {
+    kv[s] = okey(v[s]);
+    if (ok[s]) {
+      lo = kv[s] < lo ? kv[s] : lo;
+      hi = kv[s] > hi ? kv[s] : hi;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t a = (uint64_t)__shfl_xor((long long)lo, o), b = (uint64_t)__shfl_xor((long long)hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  while (lo < hi) {  // smallest key K with #(key <= K) >= k+1
+    const uint64_t mid = lo + ((hi - lo) >> 1);
+    int cnt = 0;
+#pragma unroll
+    for (int s = 0; s < MPL; ++s) cnt += __popcll(__ballot(ok[s] && kv[s] <= mid));
+    if (cnt >= k + 1)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return from_okey(lo);
+}
+
+template <int MPL>
+__device__ double score_at_percentile_f(const double (&v)[MPL], const bool (&ok)[MPL], int n,
+                                        double per) {
+  const double idx = per / 100.0 * (double)(n - 1);
+  const int i = (int)idx;
+  if ((double)i == idx) return kth_smallest_f<MPL>(v, ok, i);
+  const double w0 = (double)(i + 1) - idx, w1 = idx - (double)i;
+  const double si = kth_smallest_f<MPL>(v, ok, i);
+  const double sj = kth_smallest_f<MPL>(v, ok, i + 1);
+  return (si * w0 + sj * w1) / (w0 + w1);
+}
+
+// freedmanDiaconisRule on float data: rnge / binwidth is a true division (binwidth 60 too);
+// a NaN bin count (int(nan) raises ValueError) or one beyond int range returns -1
+template <int MPL>
+__device__ int fd_bins_f(const double (&v)[MPL], const bool (&ok)[MPL], int n, double c,
+                         double vmin, double vmax) {
+  const double iqr = score_at_percentile_f<MPL>(v, ok, n, 75.0) -
+                     score_at_percentile_f<MPL>(v, ok, n, 25.0);
+  double bw = 2.0 * iqr * c;
+  if (bw <= 0.0) bw = 60.0;
+  const double q = ceil((vmax - vmin) / bw);
+  if (!(q == q)) return -1;
+  return q > 1e9 ? 1000000000 : (int)q;
+}
+
+// numpy.histogram(data, nbins) into per-wave LDS counters
 struct HistSpec {
   double first, last, step;
   int nb;
   __device__ double edge(int i) const { return i >= nb ? last : (double)i * step + first; }
 };
 
-__device__ __forceinline__ HistSpec hist_spec(int vmin, int vmax, int nb) {
+__device__ __forceinline__ HistSpec hist_spec(double vmin, double vmax, int nb) {
   HistSpec h;
-  h.first = (double)vmin;
-  h.last = (double)vmax;
+  h.first = vmin;
+  h.last = vmax;
   if (vmin == vmax) {
     h.first -= 0.5;
     h.last += 0.5;
@@ -85,8 +157,7 @@ __device__ __forceinline__ HistSpec hist_spec(int vmin, int vmax, int nb) {
   return h;
 }
 
-__device__ __forceinline__ int hist_bin(const HistSpec& h, int iv) {
-  const double v = (double)iv;
+__device__ __forceinline__ int hist_bin(const HistSpec& h, double v) {
   const double denom = (double)(h.last - h.first);
   int idx = (int)(((v - h.first) / denom) * (double)h.nb);
   if (idx == h.nb) idx -= 1;
@@ -247,10 +318,13 @@ __device__ void load_hist(GaussFn<MPL>& fn, const int* hist, const HistSpec& h, 
   }
 }
 
-// P = slots of the profile (lp <= 64*P), H = histogram-bin slots (nb <= 64*H)
-template <int P, int H, bool BIG>
+// P = slots of the profile (lp <= 64*P), H = histogram-bin slots (nb <= 64*H);
+// F = float profiles (the PFD path): float order statistics, true-division bin counts and
+// numpy's pairwise mean / std instead of the exact integer forms
+template <int P, int H, bool BIG, bool F>
 __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   __shared__ int hist_all[BLOCK / 64][64 * H];
+  __shared__ double stage_all[BLOCK / 64][F ? 64 * P : 1];
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
   if constexpr (BIG) {
@@ -260,35 +334,75 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   const int wv = threadIdx.x >> 6;
   int* hist = hist_all[wv];
   const int lp = a.lp;
-  const uint8_t* row = a.prof + c * lp;
-  int v[P], d[P];
+  using V = typename std::conditional<F, double, int>::type;
+  V v[P], d[P];
   bool okv[P], okd[P];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int i = lane + 64 * k;
     okv[k] = i < lp;
     okd[k] = i < lp - 1;
-    v[k] = okv[k] ? (int)row[i] : 0;
-    d[k] = okd[k] ? (int)row[i] - (int)row[i + 1] : 0;  // getDerivative (:170-186)
+    if constexpr (F) {
+      const double* row = a.fprof + c * lp;
+      v[k] = okv[k] ? row[i] : 0.0;
+      d[k] = okd[k] ? row[i] - row[i + 1] : 0.0;  // getDerivative (:170-186)
+    } else {
+      const uint8_t* row = a.prof + c * lp;
+      v[k] = okv[k] ? (int)row[i] : 0;
+      d[k] = okd[k] ? (int)row[i] - (int)row[i + 1] : 0;
+    }
   }
-  int vmin = 1 << 30, vmax = -(1 << 30), dmin = 1 << 30, dmax = -(1 << 30);
+  int hb, db;
+  double vmin_d, vmax_d, dmin_d, dmax_d;
+  if constexpr (F) {
+    double vmin = INFINITY, vmax = -INFINITY, dmin = INFINITY, dmax = -INFINITY;
+    bool nan = false;
 #pragma unroll
-  for (int k = 0; k < P; ++k) {
-    if (okv[k]) {
-      vmin = min(vmin, v[k]);
-      vmax = max(vmax, v[k]);
+    for (int k = 0; k < P; ++k) {
+      if (okv[k]) {
+        nan |= !(v[k] == v[k]);
+        vmin = fmin(vmin, v[k]);
+        vmax = fmax(vmax, v[k]);
+      }
+      if (okd[k]) {
+        dmin = fmin(dmin, d[k]);
+        dmax = fmax(dmax, d[k]);
+      }
     }
-    if (okd[k]) {
-      dmin = min(dmin, d[k]);
-      dmax = max(dmax, d[k]);
+    vmin_d = wmin(vmin);
+    vmax_d = wmax(vmax);
+    dmin_d = wmin(dmin);
+    dmax_d = wmax(dmax);
+    if (__ballot(nan)) {  // numpy.histogram: autodetected range is not finite (ValueError)
+      if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
+      return;
     }
+    hb = fd_bins_f<P>(v, okv, lp, a.c_lp, vmin_d, vmax_d);        // :654
+    db = fd_bins_f<P>(d, okd, lp - 1, a.c_lp1, dmin_d, dmax_d);   // :656
+  } else {
+    int vmin = 1 << 30, vmax = -(1 << 30), dmin = 1 << 30, dmax = -(1 << 30);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      if (okv[k]) {
+        vmin = min(vmin, v[k]);
+        vmax = max(vmax, v[k]);
+      }
+      if (okd[k]) {
+        dmin = min(dmin, d[k]);
+        dmax = max(dmax, d[k]);
+      }
+    }
+    vmin = wmin_i(vmin);
+    vmax = wmax_i(vmax);
+    dmin = wmin_i(dmin);
+    dmax = wmax_i(dmax);
+    hb = fd_bins<P>(v, okv, lp, a.c_lp, vmin, vmax);        // :654
+    db = fd_bins<P>(d, okd, lp - 1, a.c_lp1, dmin, dmax);   // :656
+    vmin_d = vmin;
+    vmax_d = vmax;
+    dmin_d = dmin;
+    dmax_d = dmax;
   }
-  vmin = wmin_i(vmin);
-  vmax = wmax_i(vmax);
-  dmin = wmin_i(dmin);
-  dmax = wmax_i(dmax);
-  const int hb = fd_bins<P>(v, okv, lp, a.c_lp, vmin, vmax);        // :654
-  const int db = fd_bins<P>(d, okd, lp - 1, a.c_lp1, dmin, dmax);   // :656
   uint32_t st = 0;
   if (hb <= 0 || db <= 0) st = PFE_ST_GAUSS_FAIL;                  // histogram(bins=0) raises
   if (!st && (hb > 64 * H || db > 64 * H)) st = BIG ? PFE_ST_UNSUPPORTED : ST_DEFER_HIST;
@@ -298,7 +412,7 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     return;
   }
   // ---- derivative histogram and its fit (:657-661)
-  const HistSpec hd = hist_spec(dmin, dmax, db);
+  const HistSpec hd = hist_spec(dmin_d, dmax_d, db);
   for (int i = lane; i < db; i += 64) hist[i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -312,7 +426,7 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   const HistFit fd = fit_gaussian_hist<H>(fn, db, lane);
   // ---- profile histogram and its fits (:678-705)
   __builtin_amdgcn_wave_barrier();
-  const HistSpec hp = hist_spec(vmin, vmax, hb);
+  const HistSpec hp = hist_spec(vmin_d, vmax_d, hb);
   for (int i = lane; i < hb; i += 64) hist[i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -353,7 +467,26 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     if (fx.ok[k]) q += (fx.y[k] - mean) * (fx.y[k] - mean);
   double pf[2] = {sqrt(wsum(q) / (double)hb), cmax};
   lmdif<2, H>(fx, pf, 200 * 3);
-  const MeanStd ms = int_mean_std<P>(v, lp, lane);
+  MeanStd ms;
+  if constexpr (F) {  // profile.mean(), profile.std(): numpy pairwise sums (:724, :730)
+    double* sg = stage_all[wv];
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (okv[k]) sg[lane + 64 * k] = v[k];
+    lds_sync();
+    ms.mean = np_pairwise<4>(sg, lp, lane) / (double)lp;
+    lds_sync();
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (okv[k]) {
+        const double t = v[k] - ms.mean;
+        sg[lane + 64 * k] = t * t;
+      }
+    lds_sync();
+    ms.std = sqrt(np_pairwise<4>(sg, lp, lane) / (double)lp);
+  } else {
+    ms = int_mean_std<P>(v, lp, lane);
+  }
   if (lane == 0) {
     double* o = a.out + c * 22;
     o[4] = fabs(fx.xmax - fp.mu);          // s5 (:715)
@@ -422,7 +555,7 @@ __device__ __forceinline__ void gt1_setup(const BatesArgs& a, int64_t c, const G
     double y = 0.0;
     if (ok) {
       const int src = (i + cut) % lp;  // rotated: part2 + part1 (:1107-1109)
-      const double pv = (double)a.prof[c * lp + src];
+      const double pv = prof_at(a, c * lp + src);
       if (w.minbg > 0.0) {
         y = pv - w.minbg + w.pstd;      // :730
         if (y < 0.0) y = 0.0;
@@ -674,8 +807,8 @@ struct KeptSet {
 // positions are compacted into cx[0..m1) (LDS).  Returns m1, or -1 on the reference's
 // IndexError (then s10 = s11 = 1e6 are written and the status bit is set).
 template <int P>
-__device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, int* ys, double* cx, int (&y)[P],
-                        bool (&ok)[P]) {
+__device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, double* ys, double* cx,
+                                        double (&y)[P], bool (&ok)[P]) {
   const int lane = lane_id();
   const int L = a.lp;
   const int cut = L / 2;
@@ -683,12 +816,14 @@ __device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, int* ys, 
   for (int k = 0; k < P; ++k) {
     const int i = lane + 64 * k;
     ok[k] = i < L;
-    y[k] = ok[k] ? (int)a.prof[c * L + (ok[k] ? (i + cut) % L : 0)] : -1;
+    y[k] = ok[k] ? prof_at(a, c * L + (ok[k] ? (i + cut) % L : 0)) : -1.0;
     if (ok[k]) ys[i] = y[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  int bv = -1, bi = 1 << 30;
+  // argmax (first maximum; the profile values are >= 0)
+  double bv = -1.0;
+  int bi = 1 << 30;
 #pragma unroll
   for (int k = 0; k < P; ++k)
     if (ok[k] && y[k] > bv) {
@@ -697,7 +832,8 @@ __device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, int* ys, 
     }
 #pragma unroll
   for (int s = 1; s < 64; s <<= 1) {
-    const int ov = __shfl_xor(bv, s), oi = __shfl_xor(bi, s);
+    const double ov = __shfl_xor(bv, s);
+    const int oi = __shfl_xor(bi, s);
     if (ov > bv || (ov == bv && oi < bi)) {
       bv = ov;
       bi = oi;
@@ -814,7 +950,7 @@ __device__ __forceinline__ void peel_start(const GaussAbsBgFn<P>& fn, int nlen, 
 // subtraction of a peel pass's fit from the rotated profile y (:1389-1399; the window is
 // centred on p[2], the amplitude): new data rows into fn
 template <int P>
-__device__ __forceinline__ void peel_subtract(const int (&y)[P], const bool (&ok)[P],
+__device__ __forceinline__ void peel_subtract(const double (&y)[P], const bool (&ok)[P],
                                               const double (&p)[4], GaussAbsBgFn<P>& fn) {
   const int lane = lane_id();
   const double nfwhm = fabs(FWHM_C * p[0]);
@@ -822,7 +958,7 @@ __device__ __forceinline__ void peel_subtract(const int (&y)[P], const bool (&ok
   for (int k = 0; k < P; ++k) {
     const int i = lane + 64 * k;
     const double xi = (double)i;
-    const double yi = (double)y[k];
+    const double yi = y[k];
     double ny = yi;
     if (ok[k]) {
       const double ev = g_absbg(xi, p);
@@ -839,16 +975,16 @@ __device__ __forceinline__ void peel_subtract(const int (&y)[P], const bool (&ok
 
 template <int P>
 __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
-  __shared__ int ys_all[BLOCK / 64][64 * P];
+  __shared__ double ys_all[BLOCK / 64][64 * P];
   __shared__ double cx_all[BLOCK / 64][64 * P];
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
   if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
   const int lane = lane_id();
   const int L = a.lp;
-  int* ys = ys_all[threadIdx.x >> 6];
+  double* ys = ys_all[threadIdx.x >> 6];
   double* cx = cx_all[threadIdx.x >> 6];
-  int y[P];
+  double y[P];
   bool ok[P];
   const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
   if (m1 < 0) return;
@@ -861,7 +997,7 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
     const int r = lane + 64 * k;
     cok[k] = r < m1;
     fn.x[k] = cok[k] ? cx[r] : 0.0;
-    cy[k] = cok[k] ? (double)ys[(int)fn.x[k]] : 0.0;
+    cy[k] = cok[k] ? ys[(int)fn.x[k]] : 0.0;
     fn.y[k] = cy[k];
     fn.ok[k] = r < (m1 < 4 ? 4 : m1);  // zero padding to 4 points (:1373-1377)
   }
@@ -931,7 +1067,7 @@ template <int P>
 __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
   constexpr int FPW = BLM_FPW;
   __shared__ BlmState<4, FPW> S;
-  __shared__ int ys[64 * P];
+  __shared__ double ys[64 * P];
   __shared__ double cx[64 * P];
   __shared__ int mpad[FPW];
   const int lane = lane_id();
@@ -955,7 +1091,7 @@ __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
     for (uint64_t m = fits; m; m &= m - 1) {
       const int f = __builtin_ctzll(m);
       const int64_t c = base + f;
-      int y[P];
+      double y[P];
       bool ok[P];
       const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
       if (m1 < 0) {
@@ -968,7 +1104,7 @@ __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
         const int r = lane + 64 * k;
         const bool cok = r < m1;
         fn.x[k] = cok ? cx[r] : 0.0;
-        fn.y[k] = cok ? (double)ys[(int)fn.x[k]] : 0.0;
+        fn.y[k] = cok ? ys[(int)fn.x[k]] : 0.0;
         fn.ok[k] = r < (m1 < 4 ? 4 : m1);  // zero padding to 4 points (:1373-1377)
       }
       store_rows<P>(xs + (size_t)f * 64 * P, yv + (size_t)f * 64 * P, fn);
@@ -998,14 +1134,14 @@ __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
           for (int j = 0; j < 4; ++j) wp->dg[(pass == 8 ? 0 : 4) + j] = p[j];
         }
         if (pass == 8) continue;
-        int y[P];
+        double y[P];
         bool ok[P];
         const int cut = L / 2;
 #pragma unroll
         for (int k = 0; k < P; ++k) {
           const int i = lane + 64 * k;
           ok[k] = i < L;
-          y[k] = ok[k] ? (int)a.prof[c * L + (ok[k] ? (i + cut) % L : 0)] : -1;
+          y[k] = ok[k] ? prof_at(a, c * L + (ok[k] ? (i + cut) % L : 0)) : -1.0;
         }
         GaussAbsBgFn<P> fn;
         peel_subtract<P>(y, ok, p, fn);
@@ -1100,7 +1236,7 @@ __global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
     const int i = lane + 64 * k;
     ok[k] = i < L;
     dg.x[k] = (double)i;
-    dg.y[k] = ok[k] ? (double)a.prof[c * L + (i + cut) % L] : 0.0;
+    dg.y[k] = ok[k] ? prof_at(a, c * L + (i + cut) % L) : 0.0;
     dg.ok[k] = ok[k];
   }
   double p1[4], p2[4];
@@ -1119,18 +1255,20 @@ __global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
 template <int P>
 struct Gdg8Loader {
   const uint8_t* prof;
+  const double* fprof;
   int64_t base;
   int L, cut;
   __device__ __forceinline__ DoubleGaussFn<P> operator()(int f) const {
     DoubleGaussFn<P> dg;
     const int lane = lane_id();
-    const uint8_t* row = prof + (base + f) * L;
+    const int64_t row = (base + f) * L;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int i = lane + 64 * k;
       const bool ok = i < L;
+      const int64_t idx = row + (ok ? (i + cut) % L : 0);
       dg.x[k] = (double)i;
-      dg.y[k] = ok ? (double)row[ok ? (i + cut) % L : 0] : 0.0;
+      dg.y[k] = ok ? (fprof ? fprof[idx] : (double)prof[idx]) : 0.0;
       dg.ok[k] = ok;
     }
     return dg;
@@ -1155,7 +1293,7 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
   const uint64_t fits = __ballot(part);
   if (fits == 0) return;
   const int L = a.lp;
-  const Gdg8Loader<P> load{a.prof, base, L, L / 2};
+  const Gdg8Loader<P> load{a.prof, a.fprof, base, L, L / 2};
   blm_run<8, P, FPW>(load, S, fits, 200 * 9);
   for (uint64_t m = fits; m; m &= m - 1) {
     const int f = __builtin_ctzll(m);
@@ -1182,8 +1320,13 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const bool use_blm = !(blm_env && blm_env[0] == '0');
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
-    hipLaunchKernelGGL((k_ghist<P, 4, false>), gw(a.n), dim3(BLOCK), 0, st, a);         \
-    hipLaunchKernelGGL((k_ghist<P, 16, true>), gw(a.n), dim3(BLOCK), 0, st, a);         \
+    if (a.fprof) {                                                                      \
+      hipLaunchKernelGGL((k_ghist<P, 4, false, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
+      hipLaunchKernelGGL((k_ghist<P, 16, true, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
+    } else {                                                                            \
+      hipLaunchKernelGGL((k_ghist<P, 4, false, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
+      hipLaunchKernelGGL((k_ghist<P, 16, true, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
+    }                                                                                   \
     if (use_blm)                                                                        \
       hipLaunchKernelGGL((k_gt1b<P>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)),      \
                          dim3(64), 0, st, a);                                           \

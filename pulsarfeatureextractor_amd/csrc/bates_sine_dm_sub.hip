@@ -11,6 +11,7 @@
 //           ProfileOperations.getSubband_scores :1585-1686
 #include "bates_common.h"
 #include "lm_batch.h"
+#include "np_sum.h"
 
 namespace pfe {
 
@@ -72,14 +73,15 @@ __device__ __forceinline__ int count_peak_blocks(const uint64_t (&nz)[MPL], int 
 }
 
 template <int MPL, bool SQR>
-__device__ double sine_chisq(const int (&yi)[MPL], int lp, int lane, double amp, int maxima, double y0) {
+__device__ double sine_chisq(const double (&yi)[MPL], int lp, int lane, double amp, int maxima,
+                             double y0) {
   SineFn<MPL, SQR> fn;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) {
     const int i = lane + 64 * k;
     fn.ok[k] = i < lp;
     fn.x[k] = (double)i;
-    fn.y[k] = (double)yi[k];
+    fn.y[k] = yi[k];
   }
   fn.amp = amp;
   fn.bg = amp;
@@ -111,43 +113,96 @@ __device__ double sine_chisq(const int (&yi)[MPL], int lp, int lane, double amp,
   return wsum(s) / (double)lp;                                    // :453-458
 }
 
-template <int MPL>
+// F = float profiles (the PFD path): numpy's pairwise mean / std, the sequential Python sum
+// for s4, and the UnboundLocalError of fitSine when y[0] is NaN (:427-441)
+template <int MPL, bool F>
 __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
+  __shared__ double stage_all[BLOCK / 64][F ? 64 * MPL : 1];
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
   const int lane = lane_id();
   const int lp = a.lp;
-  int v[MPL];
-  load_row_u8<MPL>(a.prof + c * lp, lp, lane, v);
-  const MeanStd ms = int_mean_std<MPL>(v, lp, lane);
-  int vmax = -1, vmin = 1 << 30;
+  double yv[MPL];
+  double h, s4, y0;
+  MeanStd ms;
+  if constexpr (F) {
+    double* sg = stage_all[threadIdx.x >> 6];
+    const double* row = a.fprof + c * lp;
+    double mx = -INFINITY, mn = INFINITY;
+    bool nan = false;
 #pragma unroll
-  for (int k = 0; k < MPL; ++k)
-    if (lane + 64 * k < lp) {
-      vmax = max(vmax, v[k]);
-      vmin = min(vmin, v[k]);
+    for (int k = 0; k < MPL; ++k) {
+      const int i = lane + 64 * k;
+      yv[k] = (i < lp) ? row[i] : 0.0;
+      if (i < lp) {
+        sg[i] = yv[k];
+        nan |= !(yv[k] == yv[k]);
+        mx = fmax(mx, yv[k]);
+        mn = fmin(mn, yv[k]);
+      }
     }
-  vmax = wmax_i(vmax);
-  vmin = wmin_i(vmin);
-  // s4 = sum((|max-min|/2) - p_i): every partial sum is exact, so = lp*h - sum(p)
-  const double h = (double)abs(vmax - vmin) / 2.0;
-  long long s1 = 0;
+    mx = wmax(mx);
+    mn = wmin(mn);
+    if (__ballot(nan)) mx = mn = NAN;  // profile.max() / .min() propagate NaN
+    h = fabs(mx - mn) / 2.0;
+    lds_sync();
+    // s4 = sum over the profile of (|max-min|/2 - p_i), a Python loop (:246-247)
+    double t = 0.0;
+    if (lane == 0)
+      for (int i = 0; i < lp; ++i) t += h - sg[i];
+    s4 = bcast(t, 0);
+    ms.mean = np_pairwise<4>(sg, lp, lane) / (double)lp;
+    lds_sync();
 #pragma unroll
-  for (int k = 0; k < MPL; ++k)
-    if (lane + 64 * k < lp) s1 += v[k];
-  s1 = wsum_ll(s1);
-  const double s4 = (double)lp * h - (double)s1;
+    for (int k = 0; k < MPL; ++k) {
+      const int i = lane + 64 * k;
+      if (i < lp) {
+        const double d = yv[k] - ms.mean;
+        sg[i] = d * d;
+      }
+    }
+    lds_sync();
+    ms.std = sqrt(np_pairwise<4>(sg, lp, lane) / (double)lp);
+    y0 = row[0];
+    if (!(y0 == y0)) {  // phi0 never assigned: fitSine raises (Sinusoid fitting exception)
+      if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
+      return;
+    }
+  } else {
+    int v[MPL];
+    load_row_u8<MPL>(a.prof + c * lp, lp, lane, v);
+    ms = int_mean_std<MPL>(v, lp, lane);
+    int vmax = -1, vmin = 1 << 30;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+      if (lane + 64 * k < lp) {
+        vmax = max(vmax, v[k]);
+        vmin = min(vmin, v[k]);
+      }
+    vmax = wmax_i(vmax);
+    vmin = wmin_i(vmin);
+    // s4 = sum((|max-min|/2) - p_i): every partial sum is exact, so = lp*h - sum(p)
+    h = (double)abs(vmax - vmin) / 2.0;
+    long long s1 = 0;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+      if (lane + 64 * k < lp) s1 += v[k];
+    s1 = wsum_ll(s1);
+    s4 = (double)lp * h - (double)s1;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) yv[k] = (double)v[k];
+    y0 = (double)__builtin_amdgcn_readfirstlane(v[0]);
+  }
   // peaks of (p - mean) - std clipped at 0
   uint64_t nz[MPL];
 #pragma unroll
   for (int k = 0; k < MPL; ++k) {
-    const bool pos = (lane + 64 * k < lp) && (((double)v[k] - ms.mean) - ms.std > 0.0);
+    const bool pos = (lane + 64 * k < lp) && ((yv[k] - ms.mean) - ms.std > 0.0);
     nz[k] = __ballot(pos);
   }
   const int maxima = count_peak_blocks<MPL>(nz, lp);
-  const double y0 = (double)__builtin_amdgcn_readfirstlane(v[0]);
-  const double c1 = sine_chisq<MPL, false>(v, lp, lane, h, maxima, y0);
-  const double c2 = sine_chisq<MPL, true>(v, lp, lane, h, maxima, y0);
+  const double c1 = sine_chisq<MPL, false>(yv, lp, lane, h, maxima, y0);
+  const double c2 = sine_chisq<MPL, true>(yv, lp, lane, h, maxima, y0);
   if (lane == 0) {
     double* o = a.out + c * 22;
     o[0] = c1 / (double)maxima;                                   // :373 (inf/nan at 0)
@@ -768,15 +823,23 @@ __global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 grid_waves(int64_t n) { return grid_for_candidates(n); }
 
-hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
+template <bool F>
+static void launch_sine_t(const BatesArgs& a, hipStream_t st) {
   if (a.lp <= 64)
-    hipLaunchKernelGGL(k_sine<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL((k_sine<1, F>), grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else if (a.lp <= 128)
-    hipLaunchKernelGGL(k_sine<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL((k_sine<2, F>), grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else if (a.lp <= 256)
-    hipLaunchKernelGGL(k_sine<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL((k_sine<4, F>), grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else
-    hipLaunchKernelGGL(k_sine<16>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL((k_sine<16, F>), grid_waves(a.n), dim3(BLOCK), 0, st, a);
+}
+
+hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
+  if (a.fprof)
+    launch_sine_t<true>(a, st);
+  else
+    launch_sine_t<false>(a, st);
   return hipGetLastError();
 }
 

@@ -361,4 +361,73 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
   return PFE_OK;
 }
 
+int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* status,
+                    uint32_t flags) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  if (!in || !out || !status) return set_err(h, PFE_EINVAL, "pfd_bates22: null argument");
+  const int64_t n = in->n;
+  if (n < 0) return set_err(h, PFE_EINVAL, "pfd_bates22: n < 0");
+  if (n == 0) return PFE_OK;
+  if (!in->profs || !in->subfreqs || !in->scal)
+    return set_err(h, PFE_EINVAL, "pfd_bates22: null input array");
+  if (in->npart < 1 || in->nsub < 2 || in->proflen < 8 || in->proflen > 1024)
+    return set_err(h, PFE_EINVAL, "pfd_bates22: shape %dx%dx%d unsupported", in->npart, in->nsub,
+                   in->proflen);
+  if (pfe::pfd_lds_bytes(in->nsub, in->proflen) > 160 * 1024)
+    return set_err(h, PFE_EINVAL, "pfd_bates22: nsub*proflen=%d exceeds the LDS-resident limit",
+                   in->nsub * in->proflen);
+  PFE_HIP(h, hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  pfe::PfdArgs a;
+  a.npart = in->npart;
+  a.nsub = in->nsub;
+  a.L = in->proflen;
+  a.n = n;
+  const size_t work = pfe::pfd22_workspace_bytes(n, in->proflen);
+  const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
+  double* dout = out;
+  uint32_t* dstat = status;
+  size_t off = 0;
+  if (flags & PFE_FLAG_DEVICE_PTRS) {
+    int rc = ensure_scratch(h, work);
+    if (rc) return rc;
+    a.profs = in->profs;
+    a.subfreqs = in->subfreqs;
+    a.scal = in->scal;
+  } else {
+    const size_t pb = align256(np * sizeof(double));
+    const size_t fb = align256((size_t)n * in->nsub * sizeof(double));
+    const size_t cb = align256((size_t)n * PFE_PFD_NSCAL * sizeof(double));
+    const size_t ob = align256((size_t)n * 22 * sizeof(double));
+    const size_t tb = align256((size_t)n * sizeof(uint32_t));
+    int rc = ensure_scratch(h, pb + fb + cb + ob + tb + work);
+    if (rc) return rc;
+    char* base = (char*)h->scratch;
+    PFE_HIP(h, hipMemcpyAsync(base, in->profs, np * sizeof(double), hipMemcpyHostToDevice, st));
+    a.profs = (const double*)base;
+    off += pb;
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->subfreqs, (size_t)n * in->nsub * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    a.subfreqs = (const double*)(base + off);
+    off += fb;
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->scal, (size_t)n * PFE_PFD_NSCAL * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    a.scal = (const double*)(base + off);
+    off += cb;
+    dout = (double*)(base + off);
+    off += ob;
+    dstat = (uint32_t*)(base + off);
+    off += tb;
+  }
+  hipError_t e = pfe::launch_pfd22(a, dout, dstat, (char*)h->scratch + off, work, st);
+  if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "pfd_bates22 launch: %s", hipGetErrorString(e));
+  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
+    PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipStreamSynchronize(st));
+  }
+  return PFE_OK;
+}
+
 }  // extern "C"

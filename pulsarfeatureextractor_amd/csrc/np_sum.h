@@ -1,0 +1,84 @@
+// np_sum.h — numpy's own reduction orders on one wavefront (device helpers shared by the
+// PFD kernels and the float-profile variants of the 22-score kernels).
+#pragma once
+
+#include "wave.h"
+
+namespace pfe {
+
+#pragma clang fp contract(off)
+
+// ---- numpy pairwise summation ---------------------------------------------------------
+// a leaf (n <= 128): r[j] = a[j] + a[j+8] + ... over the largest multiple of 8, combined as
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the remainder in order; n < 8: 0 + a0 + a1 ...
+__device__ double np_leaf(const double* a, int n, int lane) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  const int nb = n - (n % 8);
+  double r = 0.0;
+  if (lane < 8) {
+    r = a[lane];
+    for (int i = 8 + lane; i < nb; i += 8) r += a[i];
+  }
+  const double r0 = bcast(r, 0), r1 = bcast(r, 1), r2 = bcast(r, 2), r3 = bcast(r, 3);
+  const double r4 = bcast(r, 4), r5 = bcast(r, 5), r6 = bcast(r, 6), r7 = bcast(r, 7);
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (int i = nb; i < n; ++i) res += a[i];
+  return res;
+}
+
+template <int D>
+__device__ __noinline__ double np_pairwise(const double* a, int n, int lane) {
+  if (n <= 128) return np_leaf(a, n, lane);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise<D - 1>(a, n2, lane) + np_pairwise<D - 1>(a + n2, n - n2, lane);
+}
+template <>
+__device__ __noinline__ double np_pairwise<0>(const double* a, int n, int lane) {
+  return np_leaf(a, n, lane);
+}
+
+// float32 pairwise sum of a short array (n <= 128), evaluated identically in every lane
+__device__ float np_leaf_f32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  const int nb = n - (n % 8);
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  for (int i = 8; i < nb; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (int i = nb; i < n; ++i) res += a[i];
+  return res;
+}
+
+// Python's builtin min / max over a sequence (first element wins ties and NaN)
+__device__ double py_min_seq(const double* a, int n) {
+  double m = a[0];
+  for (int i = 1; i < n; ++i)
+    if (a[i] < m) m = a[i];
+  return m;
+}
+__device__ double py_max_seq(const double* a, int n) {
+  double m = a[0];
+  for (int i = 1; i < n; ++i)
+    if (a[i] > m) m = a[i];
+  return m;
+}
+
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace pfe

@@ -17,9 +17,17 @@ struct PfdArgs {
   float* chis;      // n x PFE_PFD_NDM or null
   double* lyon8;    // n x 8 or null
   uint32_t* status;
+  // the 22-score path (pfd22.hip): scores 12-15 and 20-22 into out22 (n x 22), and the
+  // DM-fit inputs [period, snr, dm, width, dm_start, dm_end] into par22 (n x 8); both or none
+  double* out22 = nullptr;
+  double* par22 = nullptr;
 };
 
 size_t pfd_lds_bytes(int nsub, int L);
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st);
+// the 22-score chain (pfd22.hip); work: pfd22_workspace_bytes(n, L) bytes of device memory
+size_t pfd22_workspace_bytes(int64_t n, int L);
+hipError_t launch_pfd22(PfdArgs a, double* out, uint32_t* status, void* work, size_t work_bytes,
+                        hipStream_t st);
 
 }  // namespace pfe

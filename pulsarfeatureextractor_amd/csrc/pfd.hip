@@ -13,79 +13,13 @@
 // as numpy does on a float32 array.  The sub-band profiles of the candidate live in LDS.
 #include <cmath>
 
+#include "np_sum.h"
 #include "pfd.h"
 #include "wave.h"
 
 namespace pfe {
 
 #pragma clang fp contract(off)
-
-// ---- numpy pairwise summation ---------------------------------------------------------
-// a leaf (n <= 128): r[j] = a[j] + a[j+8] + ... over the largest multiple of 8, combined as
-// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the remainder in order; n < 8: 0 + a0 + a1 ...
-__device__ double np_leaf(const double* a, int n, int lane) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
-  }
-  const int nb = n - (n % 8);
-  double r = 0.0;
-  if (lane < 8) {
-    r = a[lane];
-    for (int i = 8 + lane; i < nb; i += 8) r += a[i];
-  }
-  const double r0 = bcast(r, 0), r1 = bcast(r, 1), r2 = bcast(r, 2), r3 = bcast(r, 3);
-  const double r4 = bcast(r, 4), r5 = bcast(r, 5), r6 = bcast(r, 6), r7 = bcast(r, 7);
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (int i = nb; i < n; ++i) res += a[i];
-  return res;
-}
-
-template <int D>
-__device__ __noinline__ double np_pairwise(const double* a, int n, int lane) {
-  if (n <= 128) return np_leaf(a, n, lane);
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  return np_pairwise<D - 1>(a, n2, lane) + np_pairwise<D - 1>(a + n2, n - n2, lane);
-}
-template <>
-__device__ __noinline__ double np_pairwise<0>(const double* a, int n, int lane) {
-  return np_leaf(a, n, lane);
-}
-
-// float32 pairwise sum of a short array (n <= 128), evaluated identically in every lane
-__device__ float np_leaf_f32(const float* a, int n) {
-  if (n < 8) {
-    float r = 0.0f;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
-  }
-  const int nb = n - (n % 8);
-  float r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = a[j];
-  for (int i = 8; i < nb; i += 8)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (int i = nb; i < n; ++i) res += a[i];
-  return res;
-}
-
-// Python's builtin min / max over a sequence (first element wins ties and NaN)
-__device__ double py_min_seq(const double* a, int n) {
-  double m = a[0];
-  for (int i = 1; i < n; ++i)
-    if (a[i] < m) m = a[i];
-  return m;
-}
-__device__ double py_max_seq(const double* a, int n) {
-  double m = a[0];
-  for (int i = 1; i < n; ++i)
-    if (a[i] > m) m = a[i];
-  return m;
-}
 
 __device__ __forceinline__ int pymod(long long v, int m) {
   long long r = v % m;
@@ -95,12 +29,6 @@ __device__ __forceinline__ int pymod(long long v, int m) {
 
 __device__ __forceinline__ double delay_from_dm(double dm, double f) {  // PFDOperations.py:474-488
   return f > 0.0 ? dm / (0.000241 * f * f) : 0.0;
-}
-
-__device__ __forceinline__ void lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // mean, std, skew, kurtosis of x[0..n) (LDS) as numpy.mean / numpy.std / scipy.stats.skew /
@@ -165,6 +93,230 @@ __device__ void stats4_f32(const float* a, float* tmp, int n, double (&o)[4]) {
   o[3] = zero ? NAN : (double)(m4 / (m2 * m2) - 3.0f);
 }
 
+
+// ---- the 22-score path: candidate parameters and sub-band scores ---------------------
+// CandidateFileInterface.filterScore(13|14) (CandidateFileInterface.py:97-107)
+__device__ __forceinline__ double filter_neg_pfd(double v) {
+  return (fabs(v - 0.0) > 0.000005 && v < 0.0) ? 0.0 : v;
+}
+
+// numpy.argmax of an LDS row: the first maximum, or the first NaN
+__device__ int np_argmax_seq(const double* a, int n, int shift, double sub) {
+  auto at = [&](int i) { int j = i + shift; j %= n; if (j < 0) j += n; return a[j] - sub; };
+  int bi = 0;
+  double bv = at(0);
+  if (!(bv == bv)) return 0;
+  for (int i = 1; i < n; ++i) {
+    const double v = at(i);
+    if (!(v == v)) return i;
+    if (v > bv) {
+      bv = v;
+      bi = i;
+    }
+  }
+  return bi;
+}
+
+// PFDOperations.getCandidateParameters (PFDOperations.py:130-231): the S/N of the profile
+// against the mean / variance of its bins within 3 sigma, and the width between the half-
+// maximum crossings of the profile rotated to put its peak at the centre.  The reference
+// rotates with fft_rotate (:490-500) by an integer number of bins; this is the exact
+// rotation, which pocketfft's round-off (~1e-13) can differ from only when a bin lies within
+// that of the half maximum.
+__device__ void pfd_params(const double* prof, double* tmp, int L, int lane, double& snr,
+                           double& width) {
+  const double avg = np_pairwise<12>(prof, L, lane) / (double)L;          // :130
+  for (int b = lane; b < L; b += 64) {
+    const double d = prof[b] - avg;
+    tmp[b] = d * d;
+  }
+  lds_sync();
+  const double var = np_pairwise<12>(tmp, L, lane) / (double)L;          // :131
+  lds_sync();
+  const double sigma = sqrt(var);
+  const double lo = avg - 3.0 * sigma, hi = avg + 3.0 * sigma;
+  int m = 0;                                                              // :141-146
+  for (int b0 = 0; b0 < L; b0 += 64) {
+    const int b = b0 + lane;
+    const bool keep = b < L && prof[b] > lo && prof[b] < hi;
+    const uint64_t bal = __ballot(keep);
+    if (keep) tmp[m + __popcll(bal & ((1ull << lane) - 1ull))] = prof[b];
+    m += __popcll(bal);
+  }
+  lds_sync();
+  const double avg2 = np_pairwise<12>(tmp, m, lane) / (double)m;         // :148 (empty: NaN)
+  lds_sync();
+  for (int i = lane; i < m; i += 64) {
+    const double d = tmp[i] - avg2;
+    tmp[i] = d * d;
+  }
+  lds_sync();
+  const double var2 = np_pairwise<12>(tmp, m, lane) / (double)m;         // :149
+  lds_sync();
+  const double sd2 = sqrt(var2);
+  for (int b = lane; b < L; b += 64) tmp[b] = (prof[b] - avg2) / sd2;
+  lds_sync();
+  snr = np_pairwise<12>(tmp, L, lane);                                    // :151
+  lds_sync();
+  if (snr < 0.0) snr = 0.1;                                              // :152-153
+  // width (:194-231), every lane walking the LDS row identically
+  const int peak0 = np_argmax_seq(prof, L, 0, 0.0);
+  const int shift = peak0 - L / 2;                                        // Py2 int '/'
+  const double pmin = py_min_seq(prof, L);
+  auto rot = [&](int i) { int j = (i + shift) % L; if (j < 0) j += L; return prof[j] - pmin; };
+  const int peak = np_argmax_seq(prof, L, shift, pmin);
+  double rmax = rot(0);
+  for (int i = 1; i < L; ++i)
+    if (rot(i) > rmax) rmax = rot(i);
+  const double half = rmax / 2.0;
+  int left = peak;
+  while (left > 0) {
+    if (rot(left) < half) break;
+    --left;
+  }
+  int right = peak;
+  while (right < L) {
+    if (rot(right) < half) break;
+    ++right;
+  }
+  width = (1.0 * ((double)(right - left) - 1.0)) / (double)L;           // :231
+}
+
+// Pearson correlation as numpy.corrcoef computes it (see bates_sine_dm_sub.hip)
+__device__ __forceinline__ double corr_pfd(double cxy, double cxx, double cyy) {
+  double r = (cxy / sqrt(cxx)) / sqrt(cyy);
+  if (r > 1.0) r = 1.0;
+  if (r < -1.0) r = -1.0;
+  return r;
+}
+
+// lane-strided partial sums then the wave tree (the order the PHCX kernels use for dots)
+template <typename Fn>
+__device__ __forceinline__ double wdot(int n, int lane, Fn f) {
+  double s = 0.0;
+  for (int j = lane; j < n; j += 64) s += f(j);
+  return wsum(s);
+}
+
+// PFDOperations.getSubbandParameters (PFDOperations.py:401-441): s20 / s21 from
+// ProfileOperations.getSubband_scores (ProfileOperations.py:1585-1686) over the dedispersed
+// sub-band profiles T (nsub x L, profs.sum(0), PFDFile.plot_subbands :442-456) and s22 from
+// getProfileCorr (:445-466).  T is overwritten (boxcar sums).  mb, mean, var: nsub doubles.
+// false = the reference raises (max_bin unbound, width_bins == 0, no valid pair).
+__device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, double* mb,
+                                   double* bmean, double* bvar, int NS, int L, int lane,
+                                   double width, double (&o)[3]) {
+  // s22 first, while T holds the sub-band profiles
+  const double pm = np_pairwise<12>(prof, L, lane) / (double)L;
+  for (int b = lane; b < L; b += 64) tmp[b] = prof[b] - pm;
+  lds_sync();
+  const double inv2 = 1.0 / (double)(L - 1);
+  const double pvar = wdot(L, lane, [&](int b) { return tmp[b] * tmp[b]; });
+  double integ = 0.0;
+  for (int j = 0; j < NS; ++j) {
+    const double* r = T + (size_t)j * L;
+    const double mj = np_pairwise<12>(r, L, lane) / (double)L;
+    const double d = wdot(L, lane, [&](int b) { return (r[b] - mj) * tmp[b]; });
+    const double q = wdot(L, lane, [&](int b) { return (r[b] - mj) * (r[b] - mj); });
+    const double cc = fabs(corr_pfd(d * inv2, q * inv2, pvar * inv2));
+    if (cc > 0.0055) integ += cc;                                      // :463-464, :437-439
+  }
+  lds_sync();
+  const int wb = (int)ceil(width * (double)L);                          // :1603
+  const int nw = L - wb + 1;
+  if (nw <= 0 || wb <= 0) return false;  // no windows: max_bin unbound; wb == 0: ZeroDivision
+  // boxcar sums, a Python loop per window (:1608-1617), in place of each band's row
+  bool have = false;
+  double last_mb = 0.0;
+  for (int i = 0; i < NS; ++i) {
+    double* r = T + (size_t)i * L;
+    for (int j = lane; j < nw; j += 64) {
+      double s = 0.0;
+      for (int b = 0; b < wb; ++b) s += r[j + b];
+      tmp[j] = s;
+    }
+    lds_sync();
+    // first strict maximum above -10000.0 (:1619-1628); a band without one repeats the
+    // previous band's position (max_bin is one local across the bands)
+    double bvv = -10000.0;
+    int bj = 1 << 30;
+    for (int j = lane; j < nw; j += 64)
+      if (tmp[j] > bvv) {
+        bvv = tmp[j];
+        bj = j;
+      }
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const double ov = __shfl_xor(bvv, s);
+      const int oj = __shfl_xor(bj, s);
+      if (ov > bvv || (ov == bvv && oj < bj)) {
+        bvv = ov;
+        bj = oj;
+      }
+    }
+    if (bj < (1 << 30)) {
+      have = true;
+      last_mb = (double)(bj + wb / 2);                                  // Py2 wb/2
+    }
+    if (!have) return false;
+    if (lane == 0) mb[i] = last_mb;
+    for (int j = lane; j < nw; j += 64) r[j] = tmp[j];
+    lds_sync();
+  }
+  // RMS scatter of the maxima (:1629-1651)
+  const double med = np_pairwise<12>(mb, NS, lane) / (double)NS;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i = 0; i < NS; ++i)
+    if (fabs(mb[i] - med) <= (double)wb) {
+      ++count;
+      var_med += (mb[i] - med) * (mb[i] - med);
+    }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    double mu = 0.0;
+    for (int i = 0; i < NS; ++i) mu += mb[i];
+    mu /= (double)NS;
+    var = 0.0;
+    for (int i = 0; i < NS; ++i) var += (mb[i] - mu) * (mb[i] - mu);
+    var /= (double)(NS - 1);
+  }
+  const double rms = sqrt(var) / (double)wb;
+  // mean pairwise correlation of the boxcar sums, pairs (i < k) in order (:1653-1677)
+  for (int i = 0; i < NS; ++i) {
+    double* r = T + (size_t)i * L;
+    const double m = np_pairwise<12>(r, nw, lane) / (double)nw;
+    lds_sync();
+    for (int j = lane; j < nw; j += 64) r[j] = r[j] - m;
+    lds_sync();
+    const double v = wdot(nw, lane, [&](int j) { return r[j] * r[j]; });
+    if (lane == 0) bvar[i] = v;
+  }
+  lds_sync();
+  const double inv = 1.0 / (double)(nw - 1);
+  double csum = 0.0;
+  int m = 0;
+  for (int i = 0; i < NS; ++i)
+    for (int k = i + 1; k < NS; ++k) {
+      const double* ri = T + (size_t)i * L;
+      const double* rk = T + (size_t)k * L;
+      const double d = wdot(nw, lane, [&](int j) { return ri[j] * rk[j]; });
+      const double cc = corr_pfd(d * inv, bvar[i] * inv, bvar[k] * inv);
+      if (cc == cc) {
+        csum += cc;
+        ++m;
+      }
+    }
+  if (m == 0) return false;                                             // ZeroDivisionError
+  o[0] = rms;
+  o[1] = csum / (double)m;
+  o[2] = integ;
+  (void)bmean;
+  return true;
+}
+
 __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   extern __shared__ double lds[];
   const int64_t c = blockIdx.x;
@@ -176,7 +328,8 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   double* tmp = buf + L;             // L
   double* dl = tmp + L;              // NS delays
   double* sdb = dl + NS;             // NS subdelays_bins
-  int* cum = (int*)(sdb + NS);       // NS rotations applied since the dedispersion
+  double* bv = sdb + NS;             // NS (22-score path: per-band variances)
+  int* cum = (int*)(bv + NS);        // NS rotations applied since the dedispersion
   __shared__ float chs[PFE_PFD_NDM], ftmp[PFE_PFD_NDM];
   const double* sc = a.scal + c * PFE_PFD_NSCAL;
   const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
@@ -282,11 +435,42 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
       }
     }
   }
-  if (lane == 0) a.status[c] = dm_ok ? 0u : PFE_ST_PFD_DMCURVE_FAIL;
+  uint32_t st = dm_ok ? 0u : PFE_ST_PFD_DMCURVE_FAIL;
+  if (a.out22) {
+    double snr, width;
+    pfd_params(buf, tmp, L, lane, snr, width);
+    const double period = sc[PFE_PFD_BARY_P1] * 1000.0;            // PFDOperations.py:127
+    const double span1 = dm_lo + ((dm_hi - dm_lo) * 1.0) / (double)(PFE_PFD_NDM - 1);
+    const double span_last =
+        dm_lo + ((dm_hi - dm_lo) * (double)(PFE_PFD_NDM - 1)) / (double)(PFE_PFD_NDM - 1);
+    double sb[3];
+    const bool sb_ok = pfd_subband_scores(T, buf, tmp, dl, sdb, bv, NS, L, lane, width, sb);
+    if (!sb_ok) st |= PFE_ST_SUBBAND_FAIL;
+    if (lane == 0) {
+      double* o = a.out22 + c * 22;
+      o[11] = period;                                                 // s12 (PFDFile.py:776)
+      o[12] = filter_neg_pfd(snr);                                    // s13 (:777)
+      o[13] = filter_neg_pfd(bestdm);                                 // s14 (:778)
+      o[14] = width;                                                  // s15
+      o[19] = sb[0];                                                  // s20 (:861-863)
+      o[20] = sb[1];                                                  // s21
+      o[21] = sb[2];                                                  // s22
+      double* q = a.par22 + c * 8;
+      q[0] = period;
+      q[1] = snr;
+      q[2] = bestdm;
+      q[3] = width;
+      q[4] = span1;      // float(dm_index[1])            (PFDOperations.py:337)
+      q[5] = span_last;  // float(dm_index[len - 1])
+      q[6] = 0.0;
+      q[7] = 0.0;
+    }
+  }
+  if (lane == 0) a.status[c] = st;
 }
 
 size_t pfd_lds_bytes(int nsub, int L) {
-  return ((size_t)nsub * L + 2 * (size_t)L + 2 * (size_t)nsub) * sizeof(double) +
+  return ((size_t)nsub * L + 2 * (size_t)L + 3 * (size_t)nsub) * sizeof(double) +
          (size_t)nsub * sizeof(int) + 64;
 }
 

@@ -163,5 +163,6 @@ def batch_inputs(datas):
         profs[i] = d.profs
         subfreqs[i] = d.subfreqs
         dms = np.atleast_1d(d.dms)
-        scal[i, :7] = (d.bestdm, d.binspersec, d.avgprof, d.varprof, dms[0], dms[-1], d.numdms)
+        scal[i] = (d.bestdm, d.binspersec, d.avgprof, d.varprof, dms[0], dms[-1], d.numdms,
+                   d.bary_p1)
     return profs, subfreqs, scal

@@ -126,6 +126,29 @@ def score_pfd(datas, engine=None, batch: int = 1 << 14):
     return out, profiles, err
 
 
+def score_pfd22(datas, engine=None, batch: int = 1 << 16):
+    """22 scores of parsed PFD folds on the GPU (pfe_pfd_bates22, PFDFile.compute):
+    returns (scores (n,22), error message or None per fold)."""
+    engine = engine or get_engine()
+    n = len(datas)
+    out = np.full((n, 22), np.nan)
+    err = [None] * n
+    groups: dict = {}
+    for i, d in enumerate(datas):
+        groups.setdefault((d.npart, d.nsub, d.proflen), []).append(i)
+    for _shape, idx in groups.items():
+        for s0 in range(0, len(idx), batch):
+            part = idx[s0:s0 + batch]
+            o, st = engine.pfd_bates22(*_pfd.batch_inputs([datas[i] for i in part]))
+            for j, i in enumerate(part):
+                msg = status_error(int(st[j]))
+                if msg:
+                    err[i] = msg
+                else:
+                    out[i] = o[j]
+    return out, err
+
+
 def _shape_key(c):
     return (len(c.profile), c.subbands.shape[0], c.subbands.shape[1], len(c.dm_curve))
 
@@ -213,58 +236,65 @@ class DataProcessor:
                  f"Execution time:  {end - start}")
 
     # ---- 22 scores / profile bins ---------------------------------------------------
+    def _rows(self, paths, genProfileData):
+        """{index: (row, None)} or {index: (None, error)} in discovery order: PHCX / SUPERB
+        files through the native reader and pfe_bates22, PFD files through the host reader
+        and pfe_pfd_bates22 (or the profile bins, --profile)."""
+        res = {}
+        px = [i for i, p in enumerate(paths) if not is_pfd(p)]
+        pf = [i for i, p in enumerate(paths) if is_pfd(p)]
+        if px:
+            parsed = parse_all([paths[i] for i in px], self.workers)
+            good = [k for k, (c, e) in enumerate(parsed) if c is not None]
+            cands = [parsed[k][0] for k in good]
+            if genProfileData:
+                rows = [[float(v) for v in c.profile] for c in cands]
+                errs = [None] * len(cands)
+            else:
+                sc, errs = score_bates(cands, self.engine)
+                rows = [sc[j] for j in range(len(cands))]
+            for j, k in enumerate(good):
+                res[px[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
+            for k, (c, e) in enumerate(parsed):
+                if c is None:
+                    res[px[k]] = (None, e)
+        if pf:
+            rd = [_read_pfd(paths[i]) for i in pf]
+            good = [k for k, (d, e) in enumerate(rd) if d is not None]
+            datas = [rd[k][0] for k in good]
+            if genProfileData:       # PFDFile.computeProfileScores (:479-492)
+                _f, profiles, _e = score_pfd(datas, self.engine)
+                rows = [[float(v) for v in pr] for pr in profiles]
+                errs = [None] * len(datas)
+            else:
+                sc, errs = score_pfd22(datas, self.engine)
+                rows = [sc[j] for j in range(len(datas))]
+            for j, k in enumerate(good):
+                res[pf[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
+            for k, (d, e) in enumerate(rd):
+                if d is None:
+                    res[pf[k]] = (None, e)
+        return res
+
     def processCollectively(self, directory, verbose, regexes, outPath, arff, genProfileData,
                             single):
-        if arff:
+        if arff:                                              # prepareARFFFile (:329-367)
             nattr = 22
-            if genProfileData:
-                nattr = 64 if self.superb else 128
+            if genProfileData and self.superb:
+                nattr = 64
+            elif genProfileData and self.phcx:
+                nattr = 128
             writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        if any(is_pfd(p) for p in paths):
-            if not genProfileData:
-                raise NotImplementedError("the 22-score path for PFD files is not in this build "
-                                          "(pfe_pfd_dmprof covers --dmprof and --profile)")
-            return self._pfd_profiles(paths, outPath, arff, start)
-        parsed = parse_all(paths, self.workers)
-        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
-        cands = [parsed[i][0] for i in good]
-        if genProfileData:
-            scores = [[float(v) for v in c.profile] for c in cands]
-            errs = [None] * len(cands)
-        else:
-            sc, errs = score_bates(cands, self.engine)
-            scores = [sc[j] for j in range(len(cands))]
-        res = {i: (scores[j], errs[j]) for j, i in enumerate(good)}
+        res = self._rows(paths, genProfileData)
         ok = failed = 0
         for i, p in enumerate(paths):
-            if i not in res:
-                self._fail(p, parsed[i][1])
-                failed += 1
-                continue
             s, e = res[i]
-            if e:
+            if s is None:
                 self._fail(p, e)
                 failed += 1
                 continue
-            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
-            ok += 1
-        self._finish(outPath, len(paths), ok, failed, start)
-
-    def _pfd_profiles(self, paths, outPath, arff, start):
-        """--profile for PFD files: the 0..255 profile bins (PFDFile.computeProfileScores)."""
-        rd = [_read_pfd(p) for p in paths]
-        good = [k for k, (d, e) in enumerate(rd) if d is not None]
-        _f, profiles, _e = score_pfd([rd[k][0] for k in good], self.engine)
-        prof = {k: profiles[j] for j, k in enumerate(good)}
-        ok = failed = 0
-        for i, p in enumerate(paths):
-            if i not in prof:
-                self._fail(p, rd[i][1])
-                failed += 1
-                continue
-            s = [float(v) for v in prof[i]]
             self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
             ok += 1
         self._finish(outPath, len(paths), ok, failed, start)
@@ -288,19 +318,16 @@ class DataProcessor:
                                  processSingleCandidate)
 
     def processSeparately(self, directory, verbose, regexes, single):
+        """:603-687 — each candidate's 22 scores into <candidate>.dat."""
         paths = self._candidates(directory, regexes, single)
-        parsed = parse_all(paths, self.workers)
-        good = [i for i, (c, e) in enumerate(parsed) if c is not None]
-        sc, errs = score_bates([parsed[i][0] for i in good], self.engine)
-        for j, i in enumerate(good):
-            if errs[j]:
-                self._fail(paths[i], errs[j])
+        res = self._rows(paths, False)
+        for i, p in enumerate(paths):
+            s, e = res[i]
+            if s is None:
+                self._fail(p, e)
             else:
-                with open(paths[i] + ".dat", "w") as f:                 # :442-447
-                    f.write(writers.dat_text(sc[j]))
-        for i, (c, e) in enumerate(parsed):
-            if c is None:
-                self._fail(paths[i], e)
+                with open(p + ".dat", "w") as f:                   # outputScores :429-447
+                    f.write(writers.dat_text(s))
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
         self.phcx = True
@@ -365,10 +392,24 @@ class DataProcessor:
         self.superb = True
         self.dmprof(directory, verbose, [SUPERB_RE], outPath, arff, processSingleCandidate)
 
-    # ---- not in this build -------------------------------------------------------------
-    def _pfd(self, *a, **k):
-        raise NotImplementedError("the PFD 22-score modes are not in this build yet "
-                                  "(--dmprof and --profile are)")
+    def processPFDSeparately(self, directory, verbose, processSingleCandidate):
+        self.pfd = True
+        self.processSeparately(directory, verbose, list(PFD_RES), processSingleCandidate)
 
-    processPFDSeparately = processPFDAndPHCXSeparately = processPFDAndPHCXCollectively = _pfd
-    labelPHCX = labelPFD = _pfd
+    def processPFDAndPHCXSeparately(self, directory, verbose, processSingleCandidate):
+        self.pfd = self.phcx = True
+        self.processSeparately(directory, verbose, [PHCX_RE] + list(PFD_RES),
+                               processSingleCandidate)
+
+    def processPFDAndPHCXCollectively(self, directory, verbose, outPath, arff, genProfileData,
+                                      processSingleCandidate):
+        self.pfd = self.phcx = True
+        self.processCollectively(directory, verbose, [PHCX_RE] + list(PFD_RES), outPath, arff,
+                                 genProfileData, processSingleCandidate)
+
+    # ---- not in this build -------------------------------------------------------------
+    def _label(self, *a, **k):
+        raise NotImplementedError("--label (interactive labelling, DataProcessor.py:691-826) "
+                                  "is not in this build")
+
+    labelPHCX = labelPFD = _label

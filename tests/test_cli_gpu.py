@@ -113,5 +113,19 @@ def test_pfd_dmprof_and_profile_cli(tmp_path, monkeypatch):
         ref = np.nan_to_num(g["profile"][i], nan=0.0)
         got = rows[os.path.join(base, os.path.basename(f))]
         assert got == [float("%.12g" % v) for v in ref], i
-    # the PFD 22-score mode is refused, not approximated
-    assert cli.main(["-c", str(cand), "-o", str(tmp_path / "s.csv"), "--pfd"]) == 2
+    # the 22-score mode (processPFDCollectively): same failing files, the bit-exact columns
+    out3 = str(tmp_path / "s.csv")
+    assert cli.main(["-c", str(cand), "-o", out3, "--pfd"]) == 0
+    rows = read_rows(out3)
+    assert len(rows) == int(g["bates22_ok"].sum())
+    for i, f in enumerate(files):
+        key = os.path.join(base, os.path.basename(f))
+        if not g["bates22_ok"][i]:
+            assert key not in rows
+            continue
+        for j in (2, 3, 11, 12, 13, 14, 15, 18, 19):  # tests/test_pfd22_gpu.py EXACT
+            assert rows[key][j] == float("%.12g" % g["bates22"][i][j]), (i, j)
+    # separately: one <file>.dat per scored fold (outputScores, DataProcessor.py:429-447)
+    assert cli.main(["-c", str(cand), "-o", str(tmp_path / "absent" / "x.csv"), "--pfd"]) == 0
+    dats = sorted(p for p in os.listdir(cand) if p.endswith(".dat"))
+    assert len(dats) == int(g["bates22_ok"].sum())

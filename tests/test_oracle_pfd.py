@@ -75,3 +75,44 @@ def test_reader_layout_variants(tmp_path):
             ref = got
         for a, b in zip(got, ref):
             assert np.array_equal(a, b)
+
+
+# the reference's s10 / s11 on these folds move between runs of the reference itself (last-ulp
+# numpy SIMD differences feed the 8-pass double-Gaussian peel); s17 / s18 are the PFD DM fit,
+# which a 1-ulp nudge of its start point moves in most folds (tests/golden/chaos_floor.json)
+NOISY = (9, 10, 16, 17)
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_oracle_22_matches_reference(tmp_path, name):
+    """PFDFile.compute restated (oracle/pfd.bates22_one) against the reference's 22 scores:
+    same failing folds and failing group, every other column bit-exact, the noisy columns
+    within 1e-3 on all but a few folds."""
+    from oracle import bates as ob
+
+    g = load_set(name)
+    files = build_files(tmp_path, g)
+    rows, oks = [], []
+    for i, f in enumerate(files):
+        d = pfd.read(f)
+        try:
+            rows.append(np.array(opfd.bates22_one(d)[0]))
+            oks.append(True)
+        except ob.CandidateFailure as e:
+            rows.append(np.full(22, np.nan))
+            oks.append(False)
+            group = {"sine": "Sinusoid", "gauss": "Gaussian", "params": "Candidate parameters",
+                     "dmfit": "DM curve", "subband": "Subband"}[e.group]
+            assert group in str(g["bates22_err"][i]), (i, e, g["bates22_err"][i])
+    got, ok = np.array(rows), np.array(oks)
+    assert np.array_equal(ok, g["bates22_ok"])
+    ref = g["bates22"][ok]
+    got = got[ok]
+    for j in range(22):
+        same = (got[:, j] == ref[:, j]) | (np.isnan(got[:, j]) & np.isnan(ref[:, j]))
+        if j not in NOISY:
+            assert same.all(), f"s{j + 1} rows {np.where(~same)[0]}"
+        else:
+            with np.errstate(all="ignore"):
+                rel = np.abs(got[:, j] - ref[:, j]) / np.abs(ref[:, j])
+            assert (rel[~same] > 1e-3).sum() <= 1, f"s{j + 1}: {np.sort(rel[~same])[-3:]}"
