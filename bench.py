@@ -4,7 +4,8 @@
 metric (BASELINE.json): candidates/sec of the 8-feature (Lyon) path on synthetic 128-bin
 profile + 128-bin DM rows, plus HBM GB/s vs peak.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS_PER_GPU] [--path lyon8|bates22]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS_PER_GPU]
+                  [--path lyon8|bates22|pfd|pfd22]
 
 One "step" = one pass of the hot path (pfe_lyon8_u8 through the C-ABI, device pointers,
 inputs resident in HBM) over the rank's whole batch of synthetic candidates (config 2:
@@ -46,7 +47,7 @@ def parse():
                     help="candidates per GPU (default 10M for lyon8, 1M for bates22)")
     ap.add_argument("--lp", type=int, default=128)
     ap.add_argument("--ld", type=int, default=128)
-    ap.add_argument("--path", choices=["lyon8", "bates22", "pfd"], default="lyon8")
+    ap.add_argument("--path", choices=["lyon8", "bates22", "pfd", "pfd22"], default="lyon8")
     ap.add_argument("--pfd-shape", default="16x32x128", help="npart x nsub x proflen (pfd path)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
@@ -137,6 +138,7 @@ def pfd_block(n, shape, seed):
             npart=npart, nsub=nsub, proflen=L, profs=c["profs"], bestdm=c["bestdm"],
             binspersec=c["fold_p1"] * L, avgprof=(c["profs"] / L).sum(),
             varprof=float(stats[:, :, 5].sum()), dms=c["dms"], numdms=len(c["dms"]),
+            bary_p1=c["fold_p1"],
             subfreqs=np.arange(nsub, dtype="d") * sd + (c["lofreq"] + sd - c["chan_wid"])))
     return datas
 
@@ -163,6 +165,30 @@ def cpu_baseline_pfd(shape, sample):
     }
 
 
+def cpu_baseline_pfd22(shape, sample):
+    import warnings
+
+    from oracle.bates import CandidateFailure
+    from oracle.pfd import bates22_one
+
+    datas = pfd_block(sample, shape, 4245)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        t0 = time.perf_counter()
+        for d in datas:
+            try:
+                bates22_one(d)
+            except CandidateFailure:
+                pass
+        dt = time.perf_counter() - t0
+    return {
+        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
+        "sample": f"{sample} synthetic {shape[0]}x{shape[1]}x{shape[2]} PRESTO folds through "
+                  f"the reference-equivalent numpy/scipy PFDFile.compute restatement "
+                  f"(oracle.pfd.bates22_one), {dt:.1f} s on 1 host core",
+    }
+
+
 def load_ops_per_candidate():
     p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
     try:
@@ -175,9 +201,9 @@ def load_ops_per_candidate():
 def main():
     args = parse()
     if args.n is None:
-        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "pfd": 32768}[args.path]
+        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "pfd": 32768, "pfd22": 32768}[args.path]
     if args.cpu_sample is None:
-        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "pfd": 200}[args.path]
+        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "pfd": 200, "pfd22": 60}[args.path]
     pfd_shape = tuple(int(v) for v in args.pfd_shape.split("x"))
     import torch
     import torch.distributed as dist
@@ -210,7 +236,7 @@ def main():
 
         def step():
             eng.lyon8(prof, dm, out=out)
-    elif args.path == "pfd":
+    elif args.path in ("pfd", "pfd22"):
         import numpy as np
 
         from pulsarfeatureextractor_amd import pfd as _pfd
@@ -226,8 +252,15 @@ def main():
         tp, tf, ts = tile(profs), tile(subfreqs), tile(pscal)
         del profs
 
-        def step():
-            eng.pfd_dmprof(tp, tf, ts, profile=False, chis=False, lyon8=True)
+        if args.path == "pfd":
+            def step():
+                eng.pfd_dmprof(tp, tf, ts, profile=False, chis=False, lyon8=True)
+        else:
+            out = torch.empty((n, 22), dtype=torch.float64, device=dev)
+            status = torch.empty((n,), dtype=torch.int32, device=dev)
+
+            def step():
+                eng.pfd_bates22(tp, tf, ts, out=out, status=status)
     else:
         import numpy as np
 
@@ -347,6 +380,34 @@ def main():
                 "avg_kernel_ms_max_over_ranks": kern_ms_max,
             },
         }
+    elif args.path == "pfd22":
+        npart, nsub, L = pfd_shape
+        result = {
+            "metric": "candidates/sec (PFD 22-score path)",
+            **common,
+            "dtype": "f64",
+            "config": {
+                "workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x {nsub} "
+                            f"sub-bands x {L} bins): PFDFile.compute, 22 scores "
+                            f"(pfe_pfd_bates22)",
+                "candidates_per_gpu": n,
+                "fold_shape": list(pfd_shape),
+                "parallelism": f"candidate shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "fp64-valu",
+                "achieved": None,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": None,
+                "traffic": None,
+                "note": "operation count of the PFD 22-score path not frozen yet; the "
+                        "fits are the 22-score path's (see --path bates22)",
+                "kernel": "pfe_pfd_bates22 (9 kernels, one step)",
+                "avg_step_ms": kern_ms,
+                "avg_step_ms_max_over_ranks": kern_ms_max,
+            },
+        }
     else:
         ops = load_ops_per_candidate()
         achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
@@ -395,6 +456,8 @@ def main():
             result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
         elif args.path == "pfd":
             result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
+        elif args.path == "pfd22":
+            result["cpu_baseline"] = cpu_baseline_pfd22(pfd_shape, args.cpu_sample)
         else:
             result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
     if rank == 0:

@@ -374,7 +374,7 @@ class Engine:
         return out
 
 
-    def pfd_bates22(self, profs, subfreqs, scal):
+    def pfd_bates22(self, profs, subfreqs, scal, out=None, status=None):
         """The 22 scores of PFD folds (pfe_pfd_bates22, PFDFile.compute) for a batch of one
         shape: profs (n,npart,nsub,L) f64, subfreqs (n,nsub), scal (n,PFE_PFD_NSCAL) with
         scal[:, 7] = bary_p1.  Returns (out (n,22) f64, status (n,))."""
@@ -388,15 +388,19 @@ class Engine:
             for t in (profs, subfreqs, scal):
                 if not t.is_contiguous():
                     raise ValueError("pfd_bates22: device tensors must be contiguous")
-            out = torch.empty((n, 22), dtype=torch.float64, device=profs.device)
-            status = torch.empty((n,), dtype=torch.int32, device=profs.device)
+            if out is None:
+                out = torch.empty((n, 22), dtype=torch.float64, device=profs.device)
+            if status is None:
+                status = torch.empty((n,), dtype=torch.int32, device=profs.device)
             flags = PFE_FLAG_DEVICE_PTRS
         else:
             profs = np.ascontiguousarray(profs, dtype=np.float64)
             subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
             scal = np.ascontiguousarray(scal, dtype=np.float64)
-            out = np.empty((n, 22), dtype=np.float64)
-            status = np.empty((n,), dtype=np.uint32)
+            if out is None:
+                out = np.empty((n, 22), dtype=np.float64)
+            if status is None:
+                status = np.empty((n,), dtype=np.uint32)
             flags = 0
         pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
         self._check(self.lib.pfe_pfd_bates22(self._h, C.byref(pin), _ptr(out), _ptr(status), flags))
