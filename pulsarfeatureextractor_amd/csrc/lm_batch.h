@@ -89,6 +89,8 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
                                           int f, BlmState<N, FPW>& S, int iter, int nfev) {
   const double eps = 1.4901161193847656e-08;  // sqrt(max(epsfcn, epsmch)) = 2^-26
   const int lane = lane_id();
+  LM_ADD(1, 1);
+  LM_T0(t_fd);
   double x[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) x[j] = S.x[j][f];
@@ -107,7 +109,11 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
   nfev += N;
   int ipvt[N];
   double rdiag[N], acn[N];
+  LM_T0(t_qr);
+  LM_ADD(5, t_qr - t_fd);
   qrfac<N, MPL>(fjac, ipvt, rdiag, acn);
+  LM_T0(t_qt);
+  LM_ADD(6, t_qt - t_qr);
   double diag[N];
   if (iter == 1) {
     double wa3[N];
@@ -170,6 +176,7 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
     S.iter[f] = iter;
     S.fnorm[f] = fnorm;
   }
+  LM_ADD(7, lm_clock_p() - t_qt);
 }
 
 // first visit of fit f: residuals at the start point, then the first outer iteration
@@ -343,6 +350,7 @@ __device__ __forceinline__ void blm_run(const Loader& load, BlmState<N, FPW>& S,
                                         int maxfev) {
   static_assert(FPW <= 64, "one fit per lane");
   const int lane = lane_id();
+  LM_T0(t_start);
   blm_sync();
   for (uint64_t m = fits; m; m &= m - 1) {
     const int f = __builtin_ctzll(m);
@@ -350,21 +358,38 @@ __device__ __forceinline__ void blm_run(const Loader& load, BlmState<N, FPW>& S,
     blm_init<N, MPL, FPW>(fn, f, S);
     blm_sync();
   }
+  LM_ADD(11, lm_clock_p() - t_start);
   for (;;) {
     blm_sync();
     const bool mine = lane < FPW && ((fits >> lane) & 1ull) && S.info[lane < FPW ? lane : 0] <= 0;
     if (__ballot(mine) == 0) break;
+    LM_T0(t_simt);
     if (mine) blm_simt<N, FPW>(lane, S);
     blm_sync();
     // fits still iterating after the gtol test: evaluate their trial points
     const uint64_t act = __ballot(mine && S.info[lane < FPW ? lane : 0] == 0);
+    LM_T0(t_trial);
+    LM_ADD(12, t_trial - t_simt);
+    LM_ADD(14, 1);
+    LM_ADD(15, __builtin_popcountll(__ballot(mine)));
+    LM_ADD(2, __builtin_popcountll(act));
     for (uint64_t m = act; m; m &= m - 1) {
       const int f = __builtin_ctzll(m);
       const auto fn = load(f);
       blm_trial<N, MPL, FPW>(fn, f, S, maxfev);
       blm_sync();
     }
+    LM_ADD(9, lm_clock_p() - t_trial);
   }
+  LM_ADD(0, __builtin_popcountll(fits));
+#ifdef PFE_LM_PROFILE
+  {
+    int nf = 0;
+    for (uint64_t m = fits; m; m &= m - 1) nf += S.nfev[__builtin_ctzll(m)];
+    LM_ADD(4, nf);
+  }
+#endif
+  LM_ADD(10, lm_clock_p() - t_start);
 }
 
 }  // namespace pfe

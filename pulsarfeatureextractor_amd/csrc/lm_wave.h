@@ -35,6 +35,8 @@ constexpr double DWARF = 2.2250738585072014e-308;
 //   5 fdjac2 cycles, 6 qrfac cycles, 7 Q^T f / R / gnorm cycles, 8 lmpar cycles,
 //   9 trial evaluation cycles, 10 total lmdif cycles
 #ifdef PFE_LM_PROFILE
+// (single global counter set: the atomics of many resident waves contend on it, so absolute
+// cycle counts are inflated; use the ratios and the event counts)
 static __device__ unsigned long long pfe_lm_prof[4][16];
 __device__ __forceinline__ long long lm_clock() { return clock64(); }
 template <int N>
@@ -56,6 +58,7 @@ __device__ __forceinline__ void lm_prof_add(int k, long long v) {
   }
 #define LM_T0(v) const long long v = lm_clock()
 #define LM_ADD(k, v) lm_prof_add<N>((k), (v))
+__device__ __forceinline__ long long lm_clock_p() { return clock64(); }
 #else
 #define PFE_LM_PROFILE_EXPORT(tag)
 #define LM_T0(v) \
@@ -64,6 +67,7 @@ __device__ __forceinline__ void lm_prof_add(int k, long long v) {
 #define LM_ADD(k, v) \
   do {               \
   } while (0)
+__device__ __forceinline__ long long lm_clock_p() { return 0; }
 #endif
 
 // MINPACK enorm of a replicated n-vector (sequential, with the dwarf/giant scaling)

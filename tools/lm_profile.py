@@ -31,17 +31,25 @@ def main():
 
     lib = _native.load_library(os.path.join(ROOT, "pulsarfeatureextractor_amd", "lib", "libpfe_lmprof.so"))
     _native._lib = lib  # route the Engine through the instrumented build
-    base = bates_batch(args.n, lp=128, lsb=128, seed=31)
+    blk = min(args.n, 16384)  # a synthetic block tiled to n rows (as bench.py --path bates22)
+    base = bates_batch(blk, lp=128, lsb=128, seed=31)
+    reps = (args.n + blk - 1) // blk
     t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in base.items()}
+    t = {k: v.repeat((reps,) + (1,) * (v.dim() - 1))[:args.n].contiguous() for k, v in t.items()}
     eng = _native.Engine(0)
     out = torch.empty((args.n, 22), dtype=torch.float64, device="cuda")
     st = torch.empty((args.n,), dtype=torch.int32, device="cuda")
     buf = (C.c_ulonglong * 64)()
     for tag in ("gauss", "sine_dm_sub"):
         getattr(lib, f"pfe_lmprof_{tag}")(buf, 1)
+    torch.cuda.synchronize()
+    import time
+    print(f"lm_profile: inputs ready, n={args.n}", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
     eng.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"], out, st)
     torch.cuda.synchronize()
-    res = {}
+    print(f"lm_profile: bates22 done in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    res = {"_elapsed_s_instrumented": time.perf_counter() - t0, "_n": args.n}
     for tag in ("gauss", "sine_dm_sub"):
         fn = getattr(lib, f"pfe_lmprof_{tag}")
         fn.argtypes = [C.c_void_p, C.c_int]
@@ -67,6 +75,22 @@ def main():
             per["cycles_per_iter"] = {nm[4:]: d[nm] / max(d["iters"], 1) for nm in NAMES[5:9]}
             per["cycles_per_iter"]["trial"] = d["cyc_trial"] / max(d["lmpar"], 1)
             per["cycles_per_qrsolv_call_lmpar"] = d["cyc_lmpar"] / max(d["lmpar"], 1)
+            if row[14] > 0:  # batched solver (lm_batch.h): per-wave phase cycles
+                per["batched"] = {
+                    "simt_phases": int(row[14]),
+                    "fits_per_simt_phase": row[15] / row[14],
+                    "trial_visits": int(row[2]),
+                    "outer_iters": int(row[1]),
+                    "kcyc_init": row[11] / 1e3,
+                    "kcyc_simt": row[12] / 1e3,
+                    "kcyc_trial_visits_incl_outer": row[9] / 1e3,
+                    "kcyc_outer_fdjac": row[5] / 1e3,
+                    "kcyc_outer_qrfac": row[6] / 1e3,
+                    "kcyc_outer_qtf": row[7] / 1e3,
+                    "kcyc_total": row[10] / 1e3,
+                    "cyc_per_simt_phase": row[12] / row[14],
+                    "cyc_per_outer": (row[5] + row[6] + row[7]) / max(row[1], 1),
+                }
             res[f"{tag}/N={npar}"] = per
     print(json.dumps(res, indent=1))
 
