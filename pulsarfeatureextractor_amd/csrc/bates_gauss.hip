@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "lm_batch.h"
+#include "lm_group.h"
 #include "np_sum.h"
 
 namespace pfe {
@@ -1310,6 +1311,297 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Pooled group-LM forms (lm_group.h) of the three fit kernels, for profiles of <= 128 bins:
+// persistent waves keep GLM_FPW fit slots busy from a work queue of candidates; the
+// m-parallel half of lmdif runs in 16-lane groups (4 fits at a time), the serial half one
+// fit per lane.  Data rows of the fits in group layout: row r -> group-lane r % 16, slot r / 16.
+// ---------------------------------------------------------------------------------------
+constexpr int GLM_FPW = 32;
+static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
+constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3;  // work queues (BatesArgs::counters)
+
+template <int FPW>
+struct SlotTab {
+  long long cand[FPW];  // candidate of the slot's fit, -1 = none
+  int pass[FPW];        // peel pass (k_gdgg)
+  int mpad[FPW];        // rows [0, mpad) take part (k_gdgg)
+  int ph[FPW];          // engine phase
+  int list[FPW];        // engine scratch
+};
+
+// next candidate of a work queue (whole wave; wave-uniform)
+__device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
+  unsigned c = 0;
+  if (lane_id() == 0) c = atomicAdd(ctr, 1u);
+  return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
+}
+
+// ---- s8, s9 -----------------------------------------------------------------------------
+template <int P, int FPW>
+struct Gt1Prob {
+  static constexpr int MG = 4 * P;
+  BatesArgs a;
+  SlotTab<FPW>& T;
+  int nslots;
+  __device__ __forceinline__ bool refill(int f, BlmState<4, FPW>& S) {
+    const int lane = lane_id();
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {  // s8, s9 and the T1 parameters of the fit that ended
+      GaussBgFn<P> fn;
+      gt1_setup<P>(a, c0, a.ws[c0], fn);
+      const double p[4] = {S.x[0][f], S.x[1][f], S.x[2][f], S.x[3][f]};
+      gt1_finish<P>(a, c0, fn, p);
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_GT1G);
+        if (c >= a.n) break;
+        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) continue;
+        GaussBgFn<P> fn;
+        gt1_setup<P>(a, c, a.ws[c], fn);
+        double p[4];
+        gt1_start<P>(fn, a.lp, p);
+        if (lane == 0) {
+          T.cand[f] = c;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) S.x[j][f] = p[j];
+        }
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ GaussBgFn<MG> load(int f) const {  // gt1_setup, group layout
+    GaussBgFn<MG> fn;
+    const int64_t c = T.cand[f];
+    const double minbg = a.ws[c].minbg, pstd = a.ws[c].pstd;
+    const int lp = a.lp, cut = lp / 2, gl = glane();
+#pragma unroll
+    for (int k = 0; k < MG; ++k) {
+      const int i = gl + GLM_G * k;
+      const bool ok = i < lp;
+      fn.ok[k] = ok;
+      fn.x[k] = (double)i;
+      double y = 0.0;
+      if (ok) {
+        const double pv = prof_at(a, c * lp + (i + cut) % lp);
+        if (minbg > 0.0) {
+          y = pv - minbg + pstd;
+          if (y < 0.0) y = 0.0;
+        } else {
+          y = pv;
+        }
+      }
+      fn.y[k] = y;
+    }
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 5; }
+};
+
+template <int P>
+__global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<4, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  Gt1Prob<P, FPW> prob{a, T, a.fpw};
+  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
+}
+
+// ---- s10, s11: the 8 peel passes ----------------------------------------------------------
+template <int P, int FPW>
+struct PeelProb {
+  static constexpr int MG = 4 * P;
+  BatesArgs a;
+  SlotTab<FPW>& T;
+  double* xs;  // wave scratch: x rows of the slots, [FPW][64P]
+  double* yv;  // y rows
+  double* ys;  // LDS [64P] (gdg_peel)
+  double* cx;  // LDS [64P]
+  int nslots;
+  __device__ __forceinline__ bool refill(int f, BlmState<4, FPW>& S) {
+    const int lane = lane_id();
+    const int L = a.lp;
+    double* X = xs + (size_t)f * 64 * P;
+    double* Y = yv + (size_t)f * 64 * P;
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {
+      const int ps = T.pass[f];
+      double p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = S.x[j][f];
+      if (ps >= 7 && lane == 0) {  // store_p2 (pass 7), store_p1 (pass 8) (:1402-1408)
+        GaussWS* wp = a.ws + c0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wp->dg[(ps == 8 ? 0 : 4) + j] = p[j];
+      }
+      if (ps < 8) {  // subtract this pass's fit, start the next one on all L points
+        const int cut = L / 2;
+        double y[P];
+        bool ok[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const int i = lane + 64 * k;
+          ok[k] = i < L;
+          y[k] = ok[k] ? prof_at(a, c0 * L + (ok[k] ? (i + cut) % L : 0)) : -1.0;
+        }
+        GaussAbsBgFn<P> fn;
+        peel_subtract<P>(y, ok, p, fn);
+        store_rows<P>(X, Y, fn);
+        double q[4];
+        peel_start<P>(fn, L, q);
+        if (lane == 0) {
+          T.mpad[f] = L;
+          T.pass[f] = ps + 1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) S.x[j][f] = q[j];
+        }
+        scratch_sync();
+        blm_sync();
+        return true;
+      }
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_GDGG);
+        if (c >= a.n) break;
+        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) continue;
+        double y[P];
+        bool ok[P];
+        const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
+        if (m1 < 0) continue;
+        GaussAbsBgFn<P> fn;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const int r = lane + 64 * k;
+          const bool cok = r < m1;
+          fn.x[k] = cok ? cx[r] : 0.0;
+          fn.y[k] = cok ? ys[(int)fn.x[k]] : 0.0;
+          fn.ok[k] = r < (m1 < 4 ? 4 : m1);  // zero padding to 4 points (:1373-1377)
+        }
+        store_rows<P>(X, Y, fn);
+        double p[4];
+        peel_start<P>(fn, m1, p);
+        if (lane == 0) {
+          T.mpad[f] = m1 < 4 ? 4 : m1;
+          T.cand[f] = c;
+          T.pass[f] = 1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) S.x[j][f] = p[j];
+        }
+        scratch_sync();
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ GaussAbsBgFn<MG> load(int f) const {
+    GaussAbsBgFn<MG> fn;
+    const int gl = glane();
+    const int mp = T.mpad[f];
+    const double* X = xs + (size_t)f * 64 * P;
+    const double* Y = yv + (size_t)f * 64 * P;
+#pragma unroll
+    for (int k = 0; k < MG; ++k) {
+      const int r = gl + GLM_G * k;
+      fn.x[k] = X[r];
+      fn.y[k] = Y[r];
+      fn.ok[k] = r < mp;
+    }
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 5; }
+};
+
+template <int P>
+__global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<4, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  __shared__ double ys[64 * P];
+  __shared__ double cx[64 * P];
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
+  double* yv = xs + (size_t)FPW * 64 * P;
+  PeelProb<P, FPW> prob{a, T, xs, yv, ys, cx, a.fpw};
+  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
+}
+
+// ---- s10, s11: the final 8-parameter fit ----------------------------------------------
+template <int P, int FPW>
+struct Gdg8Prob {
+  static constexpr int MG = 4 * P;
+  BatesArgs a;
+  SlotTab<FPW>& T;
+  int nslots;
+  __device__ __forceinline__ bool refill(int f, BlmState<8, FPW>& S) {
+    const int lane = lane_id();
+    const int L = a.lp;
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {
+      const DoubleGaussFn<P> dg = Gdg8Loader<P>{a.prof, a.fprof, c0, L, L / 2}(0);
+      bool ok[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) ok[k] = dg.ok[k];
+      double q8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q8[j] = S.x[j][f];
+      const GaussWS w = a.ws[c0];
+      gdg8_finish<P>(a, c0, dg, ok, q8, w);
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_GDG8G);
+        if (c >= a.n) break;
+        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) continue;
+        if (lane < 8) S.x[lane][f] = a.ws[c].dg[lane];
+        if (lane == 0) T.cand[f] = c;
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ DoubleGaussFn<MG> load(int f) const {
+    DoubleGaussFn<MG> dg;
+    const int L = a.lp, cut = L / 2, gl = glane();
+    const int64_t row = T.cand[f] * L;
+#pragma unroll
+    for (int k = 0; k < MG; ++k) {
+      const int i = gl + GLM_G * k;
+      const bool ok = i < L;
+      dg.x[k] = (double)i;
+      dg.y[k] = ok ? prof_at(a, row + (i + cut) % L) : 0.0;
+      dg.ok[k] = ok;
+    }
+    return dg;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 9; }
+};
+
+template <int P>
+__global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<8, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  Gdg8Prob<P, FPW> prob{a, T, a.fpw};
+  glm_engine<8, 4 * P, FPW>(prob, S, T.ph, T.list);
+}
+
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }
 
@@ -1318,6 +1610,10 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   // batched lmdif (lm_batch.h) unless PFE_BLM=0 selects the wave-per-fit kernels (A/B runs)
   const char* blm_env = getenv("PFE_BLM");
   const bool use_blm = !(blm_env && blm_env[0] == '0');
+  // pooled group-LM kernels (lm_group.h) for <= 128 bins unless PFE_GLM=0 (A/B runs)
+  const char* glm_env = getenv("PFE_GLM");
+  const bool use_glm = use_blm && L <= 128 && !(glm_env && glm_env[0] == '0');
+  const dim3 pool((unsigned)a.pwaves);
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
     if (a.fprof) {                                                                      \
@@ -1327,16 +1623,22 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((k_ghist<P, 4, false, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
       hipLaunchKernelGGL((k_ghist<P, 16, true, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
     }                                                                                   \
-    if (use_blm)                                                                        \
+    if (use_glm)                                                                        \
+      hipLaunchKernelGGL((k_gt1g<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                        \
+    else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gt1b<P>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)),      \
                          dim3(64), 0, st, a);                                           \
     else                                                                                \
       hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
-    if (use_blm)                                                                        \
+    if (use_glm)                                                                        \
+      hipLaunchKernelGGL((k_gdgg<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                        \
+    else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gdgb<P>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);    \
     else                                                                                \
       hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
-    if (use_blm)                                                                        \
+    if (use_glm)                                                                        \
+      hipLaunchKernelGGL((k_gdg8g<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                       \
+    else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gdg8b<P, BLM_FPW>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)), \
                          dim3(64), 0, st, a);                                           \
     else                                                                                \

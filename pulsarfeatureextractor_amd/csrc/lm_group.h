@@ -1,0 +1,442 @@
+// lm_group.h — MINPACK lmdif for a pool of fits owned by one wave, worked in 16-lane groups.
+//
+// lm_batch.h visits one fit at a time with all 64 lanes (m = 128 rows -> 2 rows per lane),
+// so every per-fit scalar step of the m-parallel half (pivot choice, Householder scaling,
+// divisions and square roots of qrfac, the step bookkeeping of a trial) and every 64-lane
+// reduction is paid once per fit by the whole wave, and a batch runs until its slowest fit
+// is done (its SIMT phases then carry few fits).  Here:
+//
+//   * a wave owns FPW fit SLOTS; the state of each lives in LDS (BlmState, [element][slot]);
+//   * the m-parallel half runs in GROUPS of G = 16 lanes (one DPP row): NG = 4 fits are
+//     worked at once, row r of a fit in group-lane r % 16, register slot r / 16; reductions
+//     are 4 DPP steps inside the row and broadcasts are row_newbcast -- no cross-row traffic;
+//   * the serial half (gtol test, lmpar, predicted reduction) runs one fit per lane (SIMT,
+//     blm_simt of lm_batch.h, unchanged);
+//   * slots are refilled as soon as their fit ends (Problem::refill, wave-cooperative), so
+//     the pool stays full until the work queue drains: no batch waits for its slowest fit.
+//
+// Each loop iteration is: refill finished slots -> O-phase (function value at x, the
+// forward-difference Jacobian, QR, Q^T f: fresh fits and accepted steps) -> SIMT phase
+// (lmpar) -> T-phase (trial point evaluation, acceptance and convergence tests).  A phase
+// hands its slots to the groups through a compacted list, NG per round.
+//
+// The arithmetic is MINPACK's (as lm_wave.h / lm_batch.h) with m-sums ordered per lane over
+// its rows and then as a butterfly over the 16 lanes: results differ from lm_batch.h only
+// in that summation order (last-bit), i.e. like any other non-sequential lmdif.
+#pragma once
+
+#include "lm_batch.h"
+
+namespace pfe {
+
+constexpr int GLM_G = 16;  // lanes per group: one DPP row
+
+enum : int { PH_EMPTY = 0, PH_INIT = 1, PH_OUTER = 2, PH_LMPAR = 3, PH_TRIAL = 4, PH_DONE = 5 };
+
+__device__ __forceinline__ int glane() { return lane_id() & (GLM_G - 1); }
+
+// sum over the 16 lanes of a DPP row; every lane of the row gets the same bits (IEEE
+// addition is commutative, so the mirrored butterflies agree)
+__device__ __forceinline__ double gsum(double v) {
+  v += dpp_f64<DPP_QUAD_XOR1>(v);
+  v += dpp_f64<DPP_QUAD_XOR2>(v);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f64<DPP_ROW_MIRROR>(v);
+  return v;
+}
+template <int K>
+__device__ __forceinline__ void gsum_from(double (&v)[K], int lo) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_QUAD_XOR1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_QUAD_XOR2>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_ROW_HALF_MIRROR>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k >= lo) v[k] += dpp_f64<DPP_ROW_MIRROR>(v[k]);
+}
+
+// value of group-lane j (row_newbcast; j folds to a constant inside unrolled loops)
+template <int J>
+__device__ __forceinline__ double nbc(double v) {
+  return __longlong_as_double(
+      __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double gbcast(double v, int j) {
+  switch (j) {
+    case 0: return nbc<0>(v);
+    case 1: return nbc<1>(v);
+    case 2: return nbc<2>(v);
+    case 3: return nbc<3>(v);
+    case 4: return nbc<4>(v);
+    case 5: return nbc<5>(v);
+    case 6: return nbc<6>(v);
+    case 7: return nbc<7>(v);
+    case 8: return nbc<8>(v);
+    case 9: return nbc<9>(v);
+    case 10: return nbc<10>(v);
+    case 11: return nbc<11>(v);
+    case 12: return nbc<12>(v);
+    case 13: return nbc<13>(v);
+    case 14: return nbc<14>(v);
+    default: return nbc<15>(v);
+  }
+}
+
+// Euclidean norm of a group-distributed m-vector (rows outside [0,m) hold 0)
+template <int MPL>
+__device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
+  double p = 0.0;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) p += f[k] * f[k];
+  return sqrt(gsum(p));
+}
+
+// qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%16, slot r/16)
+template <int N, int MPL>
+__device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
+                                        double (&acnorm)[N]) {
+  static_assert(N <= GLM_G, "diagonal rows must sit in slot 0");
+  const int gl = glane();
+  double wa[N];
+  {
+    double s[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      double p = 0.0;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k) p += a[k][j] * a[k][j];
+      s[j] = p;
+    }
+    gsum_from(s, 0);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      acnorm[j] = sqrt(s[j]);
+      rdiag[j] = acnorm[j];
+      wa[j] = acnorm[j];
+      ipvt[j] = j;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    int kmax = j;
+    double rmax = rdiag[j];
+#pragma unroll
+    for (int k = j + 1; k < N; ++k)
+      if (rdiag[k] > rmax) {
+        kmax = k;
+        rmax = rdiag[k];
+      }
+    if (kmax != j) {
+#pragma unroll
+      for (int k2 = j + 1; k2 < N; ++k2) {
+        if (kmax == k2) {
+#pragma unroll
+          for (int s = 0; s < MPL; ++s) {
+            const double t = a[s][j];
+            a[s][j] = a[s][k2];
+            a[s][k2] = t;
+          }
+          rdiag[k2] = rdiag[j];
+          wa[k2] = wa[j];
+          const int t = ipvt[j];
+          ipvt[j] = ipvt[k2];
+          ipvt[k2] = t;
+        }
+      }
+    }
+    double p = 0.0;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+      if (row_ge(gl, k, j)) p += a[k][j] * a[k][j];
+    double ajnorm = sqrt(gsum(p));
+    if (ajnorm != 0.0) {
+      if (gbcast(a[0][j], j) < 0.0) ajnorm = -ajnorm;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k)
+        if (row_ge(gl, k, j)) a[k][j] = a[k][j] / ajnorm;
+      if (gl == j) a[0][j] = a[0][j] + 1.0;
+      double d[N];
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        double q = 0.0;
+        if (c > j) {
+#pragma unroll
+          for (int k = 0; k < MPL; ++k)
+            if (row_ge(gl, k, j)) q += a[k][j] * a[k][c];
+        }
+        d[c] = q;
+      }
+      gsum_from(d, j + 1);
+      const double ajj = gbcast(a[0][j], j);
+#pragma unroll
+      for (int c = j + 1; c < N; ++c) {
+        const double temp = d[c] / ajj;
+#pragma unroll
+        for (int k = 0; k < MPL; ++k)
+          if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
+        if (rdiag[c] != 0.0) {
+          const double t2 = gbcast(a[0][c], j) / rdiag[c];
+          rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
+          const double q = rdiag[c] / wa[c];
+          if (0.05 * (q * q) <= EPSMCH) {
+            double r = 0.0;
+#pragma unroll
+            for (int k = 0; k < MPL; ++k)
+              if (row_ge(gl, k, j + 1)) r += a[k][c] * a[k][c];
+            rdiag[c] = sqrt(gsum(r));
+            wa[c] = rdiag[c];
+          }
+        }
+      }
+    }
+    rdiag[j] = -ajnorm;
+  }
+}
+
+// O-phase for slot f (one group): residuals at S.x (a fresh fit also initialises par, delta,
+// xnorm, the counters and fnorm), the forward-difference Jacobian, QR, Q^T f, R -> LDS.
+// Leaves info = -1 (the gtol test runs in the next SIMT phase).
+template <int N, int MPL, int FPW, class Fn>
+__device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>& S, bool fresh) {
+  const double eps = 1.4901161193847656e-08;  // sqrt(max(epsfcn, epsmch)) = 2^-26
+  const int gl = glane();
+  double x[N], fvec[MPL];
+  typename FnCache<Fn>::type cache;
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = S.x[j][f];
+  // the residuals at x: for an accepted step these are the trial's residuals, recomputed
+  // (same function, same operands: the same bits)
+  fn_eval<Fn, N, MPL>(fcn, x, fvec, cache);
+  int iter, nfev;
+  double fnorm;
+  if (fresh) {
+    fnorm = enorm_g(fvec);
+    iter = 1;
+    nfev = 1;
+  } else {
+    fnorm = S.fnorm[f];
+    iter = S.iter[f];
+    nfev = S.nfev[f];
+  }
+  double fjac[MPL][N], wa4[MPL];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double temp = x[j];
+    double h = eps * fabs(temp);
+    if (h == 0.0) h = eps;
+    x[j] = temp + h;
+    fn_eval_col<Fn, N, MPL>(fcn, x, j, wa4, cache);
+    x[j] = temp;
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) fjac[k][j] = (wa4[k] - fvec[k]) / h;
+  }
+  nfev += N;
+  int ipvt[N];
+  double rdiag[N], acn[N];
+  qrfac_g<N, MPL>(fjac, ipvt, rdiag, acn);
+  double diag[N];
+  double xnorm = 0.0, delta = 0.0;
+  if (iter == 1) {
+    double wa3[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      diag[j] = acn[j];
+      if (acn[j] == 0.0) diag[j] = 1.0;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) wa3[j] = diag[j] * x[j];
+    xnorm = enorm_u(wa3);
+    delta = LM_FACTOR * xnorm;
+    if (delta == 0.0) delta = LM_FACTOR;
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) diag[j] = S.diag[j][f];
+  }
+  double qtf[N];
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double ajj = gbcast(fjac[0][j], j);
+    if (ajj != 0.0) {
+      double p = 0.0;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k)
+        if (row_ge(gl, k, j)) p += fjac[k][j] * wa4[k];
+      const double sum = gsum(p);
+      const double temp = -sum / ajj;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k)
+        if (row_ge(gl, k, j)) wa4[k] = wa4[k] + fjac[k][j] * temp;
+    }
+    if (gl == j) fjac[0][j] = rdiag[j];
+    qtf[j] = gbcast(wa4[0], j);
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (gl <= j) S.r[tri_idx(0, j) + gl][f] = fjac[0][j];
+  if (gl == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      S.diag[j][f] = fmax(diag[j], acn[j]);
+      S.qtf[j][f] = qtf[j];
+      S.acn[j][f] = acn[j];
+      S.ipvt[j][f] = ipvt[j];
+    }
+    if (iter == 1) {
+      S.xnorm[f] = xnorm;
+      S.delta[f] = delta;
+    }
+    if (fresh) S.par[f] = 0.0;
+    S.info[f] = -1;
+    S.nfev[f] = nfev;
+    S.iter[f] = iter;
+    S.fnorm[f] = fnorm;
+  }
+}
+
+// T-phase for slot f (one group): evaluate the trial point, update delta/par, accept or
+// reject, convergence tests.  Returns the slot's next phase.
+template <int N, int MPL, int FPW, class Fn>
+__device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>& S, int maxfev) {
+  const int gl = glane();
+  double wa2[N], wa4[MPL];
+  typename FnCache<Fn>::type cache;
+#pragma unroll
+  for (int j = 0; j < N; ++j) wa2[j] = S.trial[j][f];
+  fn_eval<Fn, N, MPL>(fcn, wa2, wa4, cache);
+  const int nfev = S.nfev[f] + 1;
+  const double fnorm1 = enorm_g(wa4);
+  double fnorm = S.fnorm[f];
+  double delta = S.delta[f], par = S.par[f], xnorm = S.xnorm[f];
+  const double pnorm = S.pnorm[f], prered = S.prered[f], dirder = S.dirder[f];
+  const double gnorm = S.gnorm[f];
+  int iter = S.iter[f];
+  double actred = -1.0;
+  if (0.1 * fnorm1 < fnorm) {
+    const double q = fnorm1 / fnorm;
+    actred = 1.0 - q * q;
+  }
+  double temp = S.tstale[f];
+  double ratio = 0.0;
+  if (prered != 0.0) ratio = actred / prered;
+  if (ratio <= 0.25) {
+    if (actred >= 0.0) temp = 0.5;
+    if (actred < 0.0) temp = 0.5 * dirder / (dirder + 0.5 * actred);
+    if (0.1 * fnorm1 >= fnorm || temp < 0.1) temp = 0.1;
+    delta = temp * fmin(delta, pnorm / 0.1);
+    par = par / temp;
+  } else if (par == 0.0 || ratio >= 0.75) {
+    delta = pnorm / 0.5;
+    par = 0.5 * par;
+  }
+  const bool accepted = ratio >= 1e-4;
+  if (accepted) {
+    double wa3[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) wa3[j] = S.diag[j][f] * wa2[j];
+    xnorm = enorm_u(wa3);
+    fnorm = fnorm1;
+    ++iter;
+  }
+  int info = 0;
+  if (fabs(actred) <= LM_FTOL && prered <= LM_FTOL && 0.5 * ratio <= 1.0) info = 1;
+  if (delta <= LM_XTOL * xnorm) info = 2;
+  if (fabs(actred) <= LM_FTOL && prered <= LM_FTOL && 0.5 * ratio <= 1.0 && info == 2) info = 3;
+  if (info == 0) {
+    if (nfev >= maxfev) info = 5;
+    if (fabs(actred) <= EPSMCH && prered <= EPSMCH && 0.5 * ratio <= 1.0) info = 6;
+    if (delta <= EPSMCH * xnorm) info = 7;
+    if (gnorm <= EPSMCH) info = 8;
+  }
+  if (gl == 0) {
+    S.delta[f] = delta;
+    S.par[f] = par;
+    S.nfev[f] = nfev;
+    S.info[f] = info;
+    if (accepted) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) S.x[j][f] = wa2[j];
+      S.xnorm[f] = xnorm;
+      S.fnorm[f] = fnorm;
+      S.iter[f] = iter;
+    }
+  }
+  return info != 0 ? PH_DONE : accepted ? PH_OUTER : PH_LMPAR;
+}
+
+// Hand the slots of `mask` to the groups, NG = 64/16 per round; body(f) runs in the group
+// that owns slot f (lanes of other groups are masked off).
+template <class Body>
+__device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body& body) {
+  const int lane = lane_id();
+  const int cnt = __builtin_popcountll(mask);
+  if ((mask >> lane) & 1ull) list[__builtin_popcountll(mask & ((1ull << lane) - 1ull))] = lane;
+  blm_sync();
+  const int g = lane / GLM_G;
+  for (int base = 0; base < cnt; base += 64 / GLM_G) {
+    const int idx = base + g;
+    if (idx < cnt) body(list[idx]);
+  }
+  blm_sync();
+}
+
+// The engine.  Prob provides (all called by the whole wave unless noted):
+//   bool refill(int f, S)   -- finish slot f's previous fit if it had one (prob keeps that
+//                              state), then set up its next fit: start point in S.x[.][f];
+//                              false when the slot stays empty (work exhausted)
+//   Fn   load(int f) const  -- (one group) the residual functor of slot f, rows r = gl + 16k
+//   int  maxfev(int f) const
+// ph / list: LDS int[FPW] each.
+template <int N, int MPL, int FPW, class Prob>
+__device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list) {
+  static_assert(FPW <= 64, "one slot per lane in the SIMT phase");
+  const int lane = lane_id();
+  if (lane < FPW) ph[lane] = PH_DONE;  // every slot takes its first fit in the refill step
+  blm_sync();
+  for (;;) {
+    // refill slots whose fit has ended
+    const uint64_t done = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_DONE);
+    for (uint64_t m = done; m; m &= m - 1) {
+      const int f = __builtin_ctzll(m);
+      const bool got = prob.refill(f, S);
+      if (lane == 0) ph[f] = got ? PH_INIT : PH_EMPTY;
+      blm_sync();
+    }
+    blm_sync();
+    const int myph = lane < FPW ? ph[lane] : PH_EMPTY;
+    if (__ballot(myph != PH_EMPTY) == 0) break;
+    // O-phase: fresh fits and accepted steps
+    const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
+    if (mo) {
+      glm_rounds(mo, list, [&](int f) {
+        const auto fn = prob.load(f);
+        glm_outer<N, MPL, FPW>(fn, f, S, ph[f] == PH_INIT);
+      });
+      if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
+      blm_sync();
+    }
+    // SIMT phase: the gtol test after a new Jacobian, lmpar, the trial point
+    if (lane < FPW && ph[lane] == PH_LMPAR) {
+      blm_simt<N, FPW>(lane, S);
+      ph[lane] = S.info[lane] != 0 ? PH_DONE : PH_TRIAL;
+    }
+    blm_sync();
+    // T-phase
+    const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
+    if (mt) {
+      glm_rounds(mt, list, [&](int f) {
+        const auto fn = prob.load(f);
+        const int nph = glm_trial<N, MPL, FPW>(fn, f, S, prob.maxfev(f));
+        if (glane() == 0) ph[f] = nph;
+      });
+    }
+  }
+}
+
+}  // namespace pfe

@@ -92,8 +92,9 @@ def test_vs_oracle_other_lengths(engine, lp, n):
 
 def test_batched_solver_bit_identical(engine, monkeypatch):
     """The batched lmdif kernels (lm_batch.h) reproduce the wave-per-fit kernels bit for bit
-    (PFE_BLM=0 selects the latter)."""
+    (PFE_BLM=0 selects the latter; PFE_GLM=0 keeps the pooled group kernels out)."""
     b = bates_batch(200, seed=21)
+    monkeypatch.setenv("PFE_GLM", "0")
     monkeypatch.setenv("PFE_BLM", "0")
     o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     monkeypatch.setenv("PFE_BLM", "1")
@@ -125,3 +126,30 @@ def test_batch_independence(engine):
                  for i, j in zip(cuts[:-1], cuts[1:])]
         cat = np.concatenate([p[0] for p in parts])
         assert np.array_equal(np.nan_to_num(cat, nan=7.0), np.nan_to_num(full, nan=7.0))
+
+
+@pytest.mark.parametrize("lp", [128, 64])
+def test_pooled_group_solver(engine, monkeypatch, lp):
+    """The pooled group-LM kernels (lm_group.h, the default for <= 128 bins) against the
+    batched wave kernels: same failures, bit-exact columns identical, the LM outputs
+    different only in the last bits of their m-sums (so at most at the reference's own
+    1-ulp chaos rates), and every fit's result independent of the pool it ran in."""
+    b = bates_batch(600, lp=lp, lsb=lp, seed=33 + lp)
+    monkeypatch.setenv("PFE_GLM", "0")
+    o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    monkeypatch.setenv("PFE_GLM", "1")
+    o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert np.array_equal(s0, s1)
+    ok = (s0 & 0xFF) == 0
+    r = rel_err(o1[ok], o0[ok])
+    for j in BITEXACT:
+        assert (r[:, j] == 0).all(), f"s{j + 1}"
+    floor = FLOOR["bates22_phcx128"]
+    for j in range(22):
+        if j not in BITEXACT:
+            assert (r[:, j] > 1e-5).mean() <= 1.5 * floor["moved_1e-5"][j] + 0.03, f"s{j + 1}"
+    # pool independence: the same candidates in another order and batch size
+    perm = np.random.default_rng(1).permutation(len(b["prof"]))[:250]
+    o2, s2 = engine.bates22(b["prof"][perm], b["sub"][perm], b["dmcurve"][perm], b["scal"][perm])
+    assert np.array_equal(s2, s1[perm])
+    assert np.array_equal(np.nan_to_num(o2, nan=7.0), np.nan_to_num(o1[perm], nan=7.0))
