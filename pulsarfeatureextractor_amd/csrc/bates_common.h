@@ -54,6 +54,10 @@ struct BatesArgs {
 constexpr int BATES_NCOUNTERS = 16;
 constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
 constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS state size)
+constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernels (lm_group.h)
+static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
+// work queues of the pooled kernels (BatesArgs::counters)
+constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6;
 
 // rows per lane (MPL) the kernels use for a profile of lp bins
 __host__ __device__ constexpr int profile_mpl(int lp) {

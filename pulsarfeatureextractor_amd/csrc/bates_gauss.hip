@@ -1317,26 +1317,6 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
 // m-parallel half of lmdif runs in 16-lane groups (4 fits at a time), the serial half one
 // fit per lane.  Data rows of the fits in group layout: row r -> group-lane r % 16, slot r / 16.
 // ---------------------------------------------------------------------------------------
-constexpr int GLM_FPW = 32;
-static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
-constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3;  // work queues (BatesArgs::counters)
-
-template <int FPW>
-struct SlotTab {
-  long long cand[FPW];  // candidate of the slot's fit, -1 = none
-  int pass[FPW];        // peel pass (k_gdgg)
-  int mpad[FPW];        // rows [0, mpad) take part (k_gdgg)
-  int ph[FPW];          // engine phase
-  int list[FPW];        // engine scratch
-};
-
-// next candidate of a work queue (whole wave; wave-uniform)
-__device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
-  unsigned c = 0;
-  if (lane_id() == 0) c = atomicAdd(ctr, 1u);
-  return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
-}
-
 // ---- s8, s9 -----------------------------------------------------------------------------
 template <int P, int FPW>
 struct Gt1Prob {

@@ -11,6 +11,7 @@
 //           ProfileOperations.getSubband_scores :1585-1686
 #include "bates_common.h"
 #include "lm_batch.h"
+#include "lm_group.h"
 #include "np_sum.h"
 
 namespace pfe {
@@ -72,19 +73,9 @@ __device__ __forceinline__ int count_peak_blocks(const uint64_t (&nz)[MPL], int 
   return blocks + cur;
 }
 
-template <int MPL, bool SQR>
-__device__ double sine_chisq(const double (&yi)[MPL], int lp, int lane, double amp, int maxima,
-                             double y0) {
-  SineFn<MPL, SQR> fn;
-#pragma unroll
-  for (int k = 0; k < MPL; ++k) {
-    const int i = lane + 64 * k;
-    fn.ok[k] = i < lp;
-    fn.x[k] = (double)i;
-    fn.y[k] = yi[k];
-  }
-  fn.amp = amp;
-  fn.bg = amp;
+// start point of fitSine (:398-438) / fitSineSqr (:535-541)
+template <bool SQR>
+__device__ __forceinline__ void sine_start(int maxima, int lp, double amp, double y0, double (&p)[2]) {
   double f0, phi0;
   if constexpr (!SQR) {
     f0 = (double)maxima / ((double)lp - 1.0);                     // :398
@@ -101,8 +92,29 @@ __device__ double sine_chisq(const double (&yi)[MPL], int lp, int lane, double a
     else
       phi0 = (f0 != 0.0) ? -1.0 / (4.0 * f0) : -1.0 / (4.0 * 0.00000000001);
   }
-  double p[2] = {f0, phi0};
-  lmdif<2, MPL>(fn, p, 200 * 3);
+  p[0] = f0;
+  p[1] = phi0;
+}
+
+template <int MPL, bool SQR>
+__device__ __forceinline__ SineFn<MPL, SQR> sine_fn(const double (&yi)[MPL], int lp, int lane,
+                                                    double amp) {
+  SineFn<MPL, SQR> fn;
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    fn.ok[k] = i < lp;
+    fn.x[k] = (double)i;
+    fn.y[k] = yi[k];
+  }
+  fn.amp = amp;
+  fn.bg = amp;
+  return fn;
+}
+
+// mean squared residual of the fitted model (:453-458)
+template <int MPL, bool SQR>
+__device__ __forceinline__ double sine_chi(const SineFn<MPL, SQR>& fn, const double (&p)[2], int lp) {
   double s = 0.0;
 #pragma unroll
   for (int k = 0; k < MPL; ++k)
@@ -110,23 +122,35 @@ __device__ double sine_chisq(const double (&yi)[MPL], int lp, int lane, double a
       const double d = fn.y[k] - fn.model(p, k);
       s += d * d;
     }
-  return wsum(s) / (double)lp;                                    // :453-458
+  return wsum(s) / (double)lp;
 }
 
-// F = float profiles (the PFD path): numpy's pairwise mean / std, the sequential Python sum
-// for s4, and the UnboundLocalError of fitSine when y[0] is NaN (:427-441)
+template <int MPL, bool SQR>
+__device__ double sine_chisq(const double (&yi)[MPL], int lp, int lane, double amp, int maxima,
+                             double y0) {
+  const SineFn<MPL, SQR> fn = sine_fn<MPL, SQR>(yi, lp, lane, amp);
+  double p[2];
+  sine_start<SQR>(maxima, lp, amp, y0, p);
+  lmdif<2, MPL>(fn, p, 200 * 3);
+  return sine_chi<MPL, SQR>(fn, p, lp);
+}
+
+// everything of getSinusoidFittings before the fits: s4, the amplitude h = |max-min|/2, the
+// peak count, y[0]; the profile as doubles in yv (wave layout).  fail: fitSine would raise.
+struct SinePre {
+  double h, s4, y0;
+  int maxima;
+  bool fail;
+};
 template <int MPL, bool F>
-__global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
-  __shared__ double stage_all[BLOCK / 64][F ? 64 * MPL : 1];
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
+__device__ __forceinline__ SinePre sine_prologue(const BatesArgs& a, int64_t c, double* sg,
+                                                 double (&yv)[MPL]) {
   const int lane = lane_id();
   const int lp = a.lp;
-  double yv[MPL];
-  double h, s4, y0;
+  SinePre r;
+  r.fail = false;
   MeanStd ms;
   if constexpr (F) {
-    double* sg = stage_all[threadIdx.x >> 6];
     const double* row = a.fprof + c * lp;
     double mx = -INFINITY, mn = INFINITY;
     bool nan = false;
@@ -144,13 +168,13 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
     mx = wmax(mx);
     mn = wmin(mn);
     if (__ballot(nan)) mx = mn = NAN;  // profile.max() / .min() propagate NaN
-    h = fabs(mx - mn) / 2.0;
+    r.h = fabs(mx - mn) / 2.0;
     lds_sync();
     // s4 = sum over the profile of (|max-min|/2 - p_i), a Python loop (:246-247)
     double t = 0.0;
     if (lane == 0)
-      for (int i = 0; i < lp; ++i) t += h - sg[i];
-    s4 = bcast(t, 0);
+      for (int i = 0; i < lp; ++i) t += r.h - sg[i];
+    r.s4 = bcast(t, 0);
     ms.mean = np_pairwise<4>(sg, lp, lane) / (double)lp;
     lds_sync();
 #pragma unroll
@@ -163,10 +187,12 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
     }
     lds_sync();
     ms.std = sqrt(np_pairwise<4>(sg, lp, lane) / (double)lp);
-    y0 = row[0];
-    if (!(y0 == y0)) {  // phi0 never assigned: fitSine raises (Sinusoid fitting exception)
-      if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
-      return;
+    lds_sync();
+    r.y0 = row[0];
+    if (!(r.y0 == r.y0)) {  // phi0 never assigned: fitSine raises (Sinusoid fitting exception)
+      r.fail = true;
+      r.maxima = 0;
+      return r;
     }
   } else {
     int v[MPL];
@@ -182,16 +208,16 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
     vmax = wmax_i(vmax);
     vmin = wmin_i(vmin);
     // s4 = sum((|max-min|/2) - p_i): every partial sum is exact, so = lp*h - sum(p)
-    h = (double)abs(vmax - vmin) / 2.0;
+    r.h = (double)abs(vmax - vmin) / 2.0;
     long long s1 = 0;
 #pragma unroll
     for (int k = 0; k < MPL; ++k)
       if (lane + 64 * k < lp) s1 += v[k];
     s1 = wsum_ll(s1);
-    s4 = (double)lp * h - (double)s1;
+    r.s4 = (double)lp * r.h - (double)s1;
 #pragma unroll
     for (int k = 0; k < MPL; ++k) yv[k] = (double)v[k];
-    y0 = (double)__builtin_amdgcn_readfirstlane(v[0]);
+    r.y0 = (double)__builtin_amdgcn_readfirstlane(v[0]);
   }
   // peaks of (p - mean) - std clipped at 0
   uint64_t nz[MPL];
@@ -200,16 +226,161 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
     const bool pos = (lane + 64 * k < lp) && ((yv[k] - ms.mean) - ms.std > 0.0);
     nz[k] = __ballot(pos);
   }
-  const int maxima = count_peak_blocks<MPL>(nz, lp);
-  const double c1 = sine_chisq<MPL, false>(yv, lp, lane, h, maxima, y0);
-  const double c2 = sine_chisq<MPL, true>(yv, lp, lane, h, maxima, y0);
+  r.maxima = count_peak_blocks<MPL>(nz, lp);
+  return r;
+}
+
+// F = float profiles (the PFD path): numpy's pairwise mean / std, the sequential Python sum
+// for s4, and the UnboundLocalError of fitSine when y[0] is NaN (:427-441)
+template <int MPL, bool F>
+__global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
+  __shared__ double stage_all[BLOCK / 64][F ? 64 * MPL : 1];
+  const int64_t c = wave_candidate();
+  if (c >= a.n) return;
+  const int lane = lane_id();
+  const int lp = a.lp;
+  double yv[MPL];
+  const SinePre pre = sine_prologue<MPL, F>(a, c, stage_all[threadIdx.x >> 6], yv);
+  if (pre.fail) {
+    if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
+    return;
+  }
+  const double c1 = sine_chisq<MPL, false>(yv, lp, lane, pre.h, pre.maxima, pre.y0);
+  const double c2 = sine_chisq<MPL, true>(yv, lp, lane, pre.h, pre.maxima, pre.y0);
   if (lane == 0) {
     double* o = a.out + c * 22;
-    o[0] = c1 / (double)maxima;                                   // :373 (inf/nan at 0)
-    o[1] = c2 / (double)maxima;                                   // :374
-    o[2] = (double)(maxima > 0 ? maxima - 1 : 0);                 // :376 len(diff)
-    o[3] = s4;
+    o[0] = c1 / (double)pre.maxima;                               // :373 (inf/nan at 0)
+    o[1] = c2 / (double)pre.maxima;                               // :374
+    o[2] = (double)(pre.maxima > 0 ? pre.maxima - 1 : 0);         // :376 len(diff)
+    o[3] = pre.s4;
   }
+}
+
+// pooled group-LM form (lm_group.h): a slot runs a candidate's sine fit, then its sine^2 fit
+template <int MPL>
+struct SineAnyFn {  // SineFn<MPL, sqr> with the model chosen per slot
+  double x[MPL], y[MPL];
+  bool ok[MPL];
+  double amp, bg;
+  bool sqr;
+  __device__ __forceinline__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
+    const double c = TWO_PI * p[0];
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      if (ok[k]) {
+        const double s = sin(c * x[k] + p[1]);
+        f[k] = sqr ? (y[k] - (fabs(amp) * (s * s))) + fabs(bg)   // :522 (sign bug kept)
+                   : y[k] - (fabs(amp) * s + fabs(bg));          // :418
+      } else {
+        f[k] = 0.0;
+      }
+    }
+  }
+};
+
+template <int MPL, bool F, int FPW>
+struct SineProb {
+  static constexpr int MG = 4 * MPL;
+  BatesArgs a;
+  SlotTab<FPW>& T;  // d0 = h, d1 = y0, mpad = maxima, pass = 0 (sine) / 1 (sine^2)
+  double* sg;       // LDS stage (F)
+  int nslots;
+  __device__ __forceinline__ void profile(int64_t c, double (&yv)[MPL]) const {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) {
+      const int i = lane + 64 * k;
+      yv[k] = (i < a.lp) ? prof_at(a, c * a.lp + i) : 0.0;
+    }
+  }
+  __device__ __forceinline__ bool refill(int f, BlmState<2, FPW>& S) {
+    const int lane = lane_id();
+    const int lp = a.lp;
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {
+      const int stage = T.pass[f];
+      const double h = T.d0[f];
+      const int maxima = T.mpad[f];
+      const double p[2] = {S.x[0][f], S.x[1][f]};
+      double yv[MPL];
+      profile(c0, yv);
+      if (stage == 0) {
+        const double c1 = sine_chi<MPL, false>(sine_fn<MPL, false>(yv, lp, lane, h), p, lp);
+        double q[2];
+        sine_start<true>(maxima, lp, h, T.d1[f], q);
+        if (lane == 0) {
+          a.out[c0 * 22 + 0] = c1 / (double)maxima;  // :373 (inf/nan at 0)
+          T.pass[f] = 1;
+          S.x[0][f] = q[0];
+          S.x[1][f] = q[1];
+        }
+        blm_sync();
+        return true;
+      }
+      const double c2 = sine_chi<MPL, true>(sine_fn<MPL, true>(yv, lp, lane, h), p, lp);
+      if (lane == 0) a.out[c0 * 22 + 1] = c2 / (double)maxima;  // :374
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_SINEG);
+        if (c >= a.n) break;
+        double yv[MPL];
+        const SinePre pre = sine_prologue<MPL, F>(a, c, sg, yv);
+        if (pre.fail) {
+          if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
+          continue;
+        }
+        double q[2];
+        sine_start<false>(pre.maxima, lp, pre.h, pre.y0, q);
+        if (lane == 0) {
+          double* o = a.out + c * 22;
+          o[2] = (double)(pre.maxima > 0 ? pre.maxima - 1 : 0);  // :376 len(diff)
+          o[3] = pre.s4;
+          T.cand[f] = c;
+          T.pass[f] = 0;
+          T.d0[f] = pre.h;
+          T.d1[f] = pre.y0;
+          T.mpad[f] = pre.maxima;
+          S.x[0][f] = q[0];
+          S.x[1][f] = q[1];
+        }
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ SineAnyFn<MG> load(int f) const {
+    SineAnyFn<MG> fn;
+    const int64_t c = T.cand[f];
+    const int lp = a.lp, gl = glane();
+#pragma unroll
+    for (int k = 0; k < MG; ++k) {
+      const int i = gl + GLM_G * k;
+      fn.ok[k] = i < lp;
+      fn.x[k] = (double)i;
+      fn.y[k] = fn.ok[k] ? prof_at(a, c * lp + i) : 0.0;
+    }
+    fn.amp = T.d0[f];
+    fn.bg = fn.amp;
+    fn.sqr = T.pass[f] != 0;
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 3; }
+};
+
+template <int MPL, bool F>
+__global__ __launch_bounds__(64, 2) void k_sineg(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<2, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  __shared__ double stage[F ? 64 * MPL : 1];
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  SineProb<MPL, F, FPW> prob{a, T, stage, a.fpw};
+  glm_engine<2, 4 * MPL, FPW>(prob, S, T.ph, T.list);
 }
 
 // ======================================================================================
@@ -272,9 +443,10 @@ struct DMSetup {
 };
 
 // the residual functor alone (what an m-phase visit of the batched solver rebuilds)
-template <int MPL>
-__device__ __forceinline__ void dm_functor(const BatesArgs& a, int64_t c, DMFn<MPL>& fn) {
-  const int lane = lane_id();
+// rows i = lb + STRIDE*k: the wave layout (lane, 64) or the group layout (glane, 16)
+template <int MPL, int STRIDE = 64>
+__device__ __forceinline__ void dm_functor(const BatesArgs& a, int64_t c, DMFn<MPL>& fn,
+                                           int lb = lane_id()) {
   const double* sc = a.scal + c * PFE_NSCAL;
   const double period = sc[PFE_SCAL_PERIOD_MS], dm = sc[PFE_SCAL_DM],
                width = sc[PFE_SCAL_WIDTH], dm_start = sc[PFE_SCAL_DM_START],
@@ -286,7 +458,7 @@ __device__ __forceinline__ void dm_functor(const BatesArgs& a, int64_t c, DMFn<M
   fn.period = period;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) {
-    const int i = lane + 64 * k;
+    const int i = lb + STRIDE * k;
     fn.ok[k] = i < n;
     fn.y[k] = fn.ok[k] ? a.dmcurve[c * n + (fn.ok[k] ? i : 0)] : 0.0;
     fn.x[k] = dm_start + (double)(128 * i - 1) * step;               // :196 (x = 128k-1)
@@ -395,6 +567,60 @@ __global__ __launch_bounds__(64) void k_dmfitb(BatesArgs a) {
     const double p[3] = {S.x[0][f], S.x[1][f], S.x[2][f]};
     dm_finish<MPL>(a, base + f, d, p);
   }
+}
+
+// pooled group-LM form (lm_group.h): persistent waves keep GLM_FPW DM fits in flight
+template <int MPL, int FPW>
+struct DMProb {
+  static constexpr int MG = 4 * MPL;  // rows per lane of a 16-lane group
+  BatesArgs a;
+  SlotTab<FPW>& T;
+  int nslots;
+  __device__ __forceinline__ bool refill(int f, BlmState<3, FPW>& S) {
+    const int lane = lane_id();
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {
+      DMSetup<MPL> d;
+      dm_setup<MPL>(a, c0, d);
+      const double p[3] = {S.x[0][f], S.x[1][f], S.x[2][f]};
+      dm_finish<MPL>(a, c0, d, p);
+    }
+    if (f < nslots) {
+      const int64_t c = queue_next(a.counters + CTR_DMG);
+      if (c < a.n) {
+        DMSetup<MPL> d;
+        dm_setup<MPL>(a, c, d);
+        if (lane == 0) {
+          T.cand[f] = c;
+          S.x[0][f] = d.amp0;
+          S.x[1][f] = 1.0;
+          S.x[2][f] = 0.0;
+        }
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ DMFn<MG> load(int f) const {
+    DMFn<MG> fn;
+    dm_functor<MG, GLM_G>(a, T.cand[f], fn, glane());
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 4; }
+};
+
+template <int MPL>
+__global__ __launch_bounds__(64, 2) void k_dmfitg(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<3, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  DMProb<MPL, FPW> prob{a, T, a.fpw};
+  glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list);
 }
 
 // ======================================================================================
@@ -823,8 +1049,22 @@ __global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 grid_waves(int64_t n) { return grid_for_candidates(n); }
 
+// pooled group-LM kernels (lm_group.h) unless PFE_GLM=0 or PFE_BLM=0 (A/B runs)
+static bool glm_on() {
+  const char* g = getenv("PFE_GLM");
+  const char* b = getenv("PFE_BLM");
+  return !(g && g[0] == '0') && !(b && b[0] == '0');
+}
+
 template <bool F>
 static void launch_sine_t(const BatesArgs& a, hipStream_t st) {
+  if (glm_on() && a.lp <= 128) {
+    if (a.lp <= 64)
+      hipLaunchKernelGGL((k_sineg<1, F>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_sineg<2, F>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+    return;
+  }
   if (a.lp <= 64)
     hipLaunchKernelGGL((k_sine<1, F>), grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else if (a.lp <= 128)
@@ -845,6 +1085,13 @@ hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
 
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
   const char* blm_env = getenv("PFE_BLM");
+  if (glm_on() && a.ndm <= 128) {
+    if (a.ndm <= 64)
+      hipLaunchKernelGGL(k_dmfitg<1>, dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_dmfitg<2>, dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+    return hipGetLastError();
+  }
   if (!(blm_env && blm_env[0] == '0')) {  // batched lmdif (lm_batch.h)
     const dim3 g((unsigned)((a.n + a.fpw - 1) / a.fpw));
     if (a.ndm <= 64)

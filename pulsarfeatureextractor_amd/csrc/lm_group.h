@@ -370,6 +370,25 @@ __device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>&
   return info != 0 ? PH_DONE : accepted ? PH_OUTER : PH_LMPAR;
 }
 
+// Per-slot bookkeeping of a pooled kernel (LDS): the candidate a slot works on, the stage
+// of its fit sequence and a few per-fit values; ph/list belong to the engine.
+template <int FPW>
+struct SlotTab {
+  long long cand[FPW];  // candidate of the slot's fit, -1 = none
+  int pass[FPW];        // stage of the candidate's fit sequence
+  int mpad[FPW];        // rows [0, mpad) take part
+  double d0[FPW], d1[FPW], d2[FPW];  // per-fit values of the problem
+  int ph[FPW];          // engine phase
+  int list[FPW];        // engine scratch
+};
+
+// next item of a work queue (whole wave; wave-uniform)
+__device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
+  unsigned c = 0;
+  if (lane_id() == 0) c = atomicAdd(ctr, 1u);
+  return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
+}
+
 // Hand the slots of `mask` to the groups, NG = 64/16 per round; body(f) runs in the group
 // that owns slot f (lanes of other groups are masked off).
 template <class Body>
