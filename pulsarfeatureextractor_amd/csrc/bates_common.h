@@ -18,6 +18,7 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
 // internal status bits (not exported)
 constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
+constexpr uint32_t ST_DEFER_HIST64 = 0x20000u;  // > 64 bins: the pooled histogram kernels pass it on
 
 // per-candidate workspace passed between the Gaussian-group kernels
 struct GaussWS {
@@ -25,8 +26,11 @@ struct GaussWS {
   double minbg;     // min(p_mu, mean(profile))                          (:724)
   double pstd;      // profile.std()
   double t1[4];     // fitGaussianT1 parameters (sigma, mu, A, bg)       (:739, :1246)
-  double pad;
+  double fd_mu;     // mu of the derivative-histogram fit (pooled histogram kernels)
   double dg[8];     // store_p1 ++ store_p2 of fitDoubleGaussian's passes 8 and 7 (:1402-1408)
+  double fp_amp;    // amplitude of the profile-histogram fit (pooled histogram kernels)
+  double h_min, h_max;  // profile histogram range and bin count (pooled histogram kernels)
+  int hb;
 };
 
 struct BatesArgs {
@@ -57,7 +61,8 @@ constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS s
 constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernels (lm_group.h)
 static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
 // work queues of the pooled kernels (BatesArgs::counters)
-constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6;
+constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6,
+              CTR_GHISTG = 7, CTR_GFIXG = 8;
 
 // rows per lane (MPL) the kernels use for a profile of lp bins
 __host__ __device__ constexpr int profile_mpl(int lp) {

@@ -319,10 +319,142 @@ __device__ void load_hist(GaussFn<MPL>& fn, const int* hist, const HistSpec& h, 
   }
 }
 
+// The profile, its derivative (getDerivative :170-186) and their Freedman-Diaconis bin
+// counts (:654-656) for candidate c.  F = float profiles (the PFD path): float order
+// statistics and true-division bin counts; nan = the profile holds a NaN (numpy.histogram
+// raises on the non-finite range).
+template <int P, bool F>
+struct GhPre {
+  using V = typename std::conditional<F, double, int>::type;
+  V v[P], d[P];
+  bool okv[P], okd[P];
+  int hb, db;
+  double vmin, vmax, dmin, dmax;
+  bool nan;
+};
+
+template <int P, bool F>
+__device__ __forceinline__ void ghist_prologue(const BatesArgs& a, int64_t c, GhPre<P, F>& g) {
+  const int lane = lane_id();
+  const int lp = a.lp;
+  g.nan = false;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int i = lane + 64 * k;
+    g.okv[k] = i < lp;
+    g.okd[k] = i < lp - 1;
+    if constexpr (F) {
+      const double* row = a.fprof + c * lp;
+      g.v[k] = g.okv[k] ? row[i] : 0.0;
+      g.d[k] = g.okd[k] ? row[i] - row[i + 1] : 0.0;  // getDerivative (:170-186)
+    } else {
+      const uint8_t* row = a.prof + c * lp;
+      g.v[k] = g.okv[k] ? (int)row[i] : 0;
+      g.d[k] = g.okd[k] ? (int)row[i] - (int)row[i + 1] : 0;
+    }
+  }
+  if constexpr (F) {
+    double vmin = INFINITY, vmax = -INFINITY, dmin = INFINITY, dmax = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      if (g.okv[k]) {
+        nan |= !(g.v[k] == g.v[k]);
+        vmin = fmin(vmin, g.v[k]);
+        vmax = fmax(vmax, g.v[k]);
+      }
+      if (g.okd[k]) {
+        dmin = fmin(dmin, g.d[k]);
+        dmax = fmax(dmax, g.d[k]);
+      }
+    }
+    g.vmin = wmin(vmin);
+    g.vmax = wmax(vmax);
+    g.dmin = wmin(dmin);
+    g.dmax = wmax(dmax);
+    if (__ballot(nan)) {
+      g.nan = true;
+      g.hb = g.db = 0;
+      return;
+    }
+    g.hb = fd_bins_f<P>(g.v, g.okv, lp, a.c_lp, g.vmin, g.vmax);        // :654
+    g.db = fd_bins_f<P>(g.d, g.okd, lp - 1, a.c_lp1, g.dmin, g.dmax);   // :656
+  } else {
+    int vmin = 1 << 30, vmax = -(1 << 30), dmin = 1 << 30, dmax = -(1 << 30);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      if (g.okv[k]) {
+        vmin = min(vmin, g.v[k]);
+        vmax = max(vmax, g.v[k]);
+      }
+      if (g.okd[k]) {
+        dmin = min(dmin, g.d[k]);
+        dmax = max(dmax, g.d[k]);
+      }
+    }
+    vmin = wmin_i(vmin);
+    vmax = wmax_i(vmax);
+    dmin = wmin_i(dmin);
+    dmax = wmax_i(dmax);
+    g.hb = fd_bins<P>(g.v, g.okv, lp, a.c_lp, vmin, vmax);        // :654
+    g.db = fd_bins<P>(g.d, g.okd, lp - 1, a.c_lp1, dmin, dmax);   // :656
+    g.vmin = vmin;
+    g.vmax = vmax;
+    g.dmin = dmin;
+    g.dmax = dmax;
+  }
+}
+
+// numpy.histogram counts of val[ok] into LDS hist[0, h.nb)
+template <int P, class V>
+__device__ __forceinline__ void build_hist(int* hist, const HistSpec& h, const V (&val)[P],
+                                           const bool (&ok)[P]) {
+  const int lane = lane_id();
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < h.nb; i += 64) hist[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k]) atomicAdd(&hist[hist_bin(h, val[k])], 1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// profile.mean(), profile.std() (:724, :730): exact integer sums, or numpy's pairwise sums
+// of a float profile (sg: LDS stage of 64P doubles)
+template <int P, bool F>
+__device__ __forceinline__ MeanStd ghist_meanstd(const GhPre<P, F>& g, int lp, double* sg) {
+  const int lane = lane_id();
+  MeanStd ms;
+  if constexpr (F) {
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (g.okv[k]) sg[lane + 64 * k] = g.v[k];
+    lds_sync();
+    ms.mean = np_pairwise<4>(sg, lp, lane) / (double)lp;
+    lds_sync();
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      if (g.okv[k]) {
+        const double t = g.v[k] - ms.mean;
+        sg[lane + 64 * k] = t * t;
+      }
+    lds_sync();
+    ms.std = sqrt(np_pairwise<4>(sg, lp, lane) / (double)lp);
+    lds_sync();
+  } else {
+    ms = int_mean_std<P>(g.v, lp, lane);
+  }
+  return ms;
+}
+
 // P = slots of the profile (lp <= 64*P), H = histogram-bin slots (nb <= 64*H);
+// BIG: only candidates deferred with ST_DEFER_HIST (more than 256 bins);
+// D64: only candidates the pooled kernels deferred with ST_DEFER_HIST64 (more than 64 bins);
 // F = float profiles (the PFD path): float order statistics, true-division bin counts and
 // numpy's pairwise mean / std instead of the exact integer forms
-template <int P, int H, bool BIG, bool F>
+template <int P, int H, bool BIG, bool F, bool D64 = false>
 __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   __shared__ int hist_all[BLOCK / 64][64 * H];
   __shared__ double stage_all[BLOCK / 64][F ? 64 * P : 1];
@@ -331,79 +463,21 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   if constexpr (BIG) {
     if (!(a.status[c] & ST_DEFER_HIST)) return;
   }
+  if constexpr (D64) {
+    if (!(a.status[c] & ST_DEFER_HIST64)) return;
+  }
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   int* hist = hist_all[wv];
   const int lp = a.lp;
-  using V = typename std::conditional<F, double, int>::type;
-  V v[P], d[P];
-  bool okv[P], okd[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int i = lane + 64 * k;
-    okv[k] = i < lp;
-    okd[k] = i < lp - 1;
-    if constexpr (F) {
-      const double* row = a.fprof + c * lp;
-      v[k] = okv[k] ? row[i] : 0.0;
-      d[k] = okd[k] ? row[i] - row[i + 1] : 0.0;  // getDerivative (:170-186)
-    } else {
-      const uint8_t* row = a.prof + c * lp;
-      v[k] = okv[k] ? (int)row[i] : 0;
-      d[k] = okd[k] ? (int)row[i] - (int)row[i + 1] : 0;
-    }
+  GhPre<P, F> g;
+  ghist_prologue<P, F>(a, c, g);
+  if (D64 && lane == 0) a.status[c] &= ~ST_DEFER_HIST64;
+  if (g.nan) {  // numpy.histogram: autodetected range is not finite (ValueError)
+    if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
+    return;
   }
-  int hb, db;
-  double vmin_d, vmax_d, dmin_d, dmax_d;
-  if constexpr (F) {
-    double vmin = INFINITY, vmax = -INFINITY, dmin = INFINITY, dmax = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      if (okv[k]) {
-        nan |= !(v[k] == v[k]);
-        vmin = fmin(vmin, v[k]);
-        vmax = fmax(vmax, v[k]);
-      }
-      if (okd[k]) {
-        dmin = fmin(dmin, d[k]);
-        dmax = fmax(dmax, d[k]);
-      }
-    }
-    vmin_d = wmin(vmin);
-    vmax_d = wmax(vmax);
-    dmin_d = wmin(dmin);
-    dmax_d = wmax(dmax);
-    if (__ballot(nan)) {  // numpy.histogram: autodetected range is not finite (ValueError)
-      if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
-      return;
-    }
-    hb = fd_bins_f<P>(v, okv, lp, a.c_lp, vmin_d, vmax_d);        // :654
-    db = fd_bins_f<P>(d, okd, lp - 1, a.c_lp1, dmin_d, dmax_d);   // :656
-  } else {
-    int vmin = 1 << 30, vmax = -(1 << 30), dmin = 1 << 30, dmax = -(1 << 30);
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      if (okv[k]) {
-        vmin = min(vmin, v[k]);
-        vmax = max(vmax, v[k]);
-      }
-      if (okd[k]) {
-        dmin = min(dmin, d[k]);
-        dmax = max(dmax, d[k]);
-      }
-    }
-    vmin = wmin_i(vmin);
-    vmax = wmax_i(vmax);
-    dmin = wmin_i(dmin);
-    dmax = wmax_i(dmax);
-    hb = fd_bins<P>(v, okv, lp, a.c_lp, vmin, vmax);        // :654
-    db = fd_bins<P>(d, okd, lp - 1, a.c_lp1, dmin, dmax);   // :656
-    vmin_d = vmin;
-    vmax_d = vmax;
-    dmin_d = dmin;
-    dmax_d = dmax;
-  }
+  const int hb = g.hb, db = g.db;
   uint32_t st = 0;
   if (hb <= 0 || db <= 0) st = PFE_ST_GAUSS_FAIL;                  // histogram(bins=0) raises
   if (!st && (hb > 64 * H || db > 64 * H)) st = BIG ? PFE_ST_UNSUPPORTED : ST_DEFER_HIST;
@@ -413,29 +487,14 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     return;
   }
   // ---- derivative histogram and its fit (:657-661)
-  const HistSpec hd = hist_spec(dmin_d, dmax_d, db);
-  for (int i = lane; i < db; i += 64) hist[i] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int k = 0; k < P; ++k)
-    if (okd[k]) atomicAdd(&hist[hist_bin(hd, d[k])], 1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  const HistSpec hd = hist_spec(g.dmin, g.dmax, db);
+  build_hist<P>(hist, hd, g.d, g.okd);
   GaussFn<H> fn;
   load_hist<H>(fn, hist, hd, lane);
   const HistFit fd = fit_gaussian_hist<H>(fn, db, lane);
   // ---- profile histogram and its fits (:678-705)
-  __builtin_amdgcn_wave_barrier();
-  const HistSpec hp = hist_spec(vmin_d, vmax_d, hb);
-  for (int i = lane; i < hb; i += 64) hist[i] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int k = 0; k < P; ++k)
-    if (okv[k]) atomicAdd(&hist[hist_bin(hp, v[k])], 1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  const HistSpec hp = hist_spec(g.vmin, g.vmax, hb);
+  build_hist<P>(hist, hp, g.v, g.okv);
   load_hist<H>(fn, hist, hp, lane);
   GaussFixedFn<H> fx;
 #pragma unroll
@@ -468,26 +527,7 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     if (fx.ok[k]) q += (fx.y[k] - mean) * (fx.y[k] - mean);
   double pf[2] = {sqrt(wsum(q) / (double)hb), cmax};
   lmdif<2, H>(fx, pf, 200 * 3);
-  MeanStd ms;
-  if constexpr (F) {  // profile.mean(), profile.std(): numpy pairwise sums (:724, :730)
-    double* sg = stage_all[wv];
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-      if (okv[k]) sg[lane + 64 * k] = v[k];
-    lds_sync();
-    ms.mean = np_pairwise<4>(sg, lp, lane) / (double)lp;
-    lds_sync();
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-      if (okv[k]) {
-        const double t = v[k] - ms.mean;
-        sg[lane + 64 * k] = t * t;
-      }
-    lds_sync();
-    ms.std = sqrt(np_pairwise<4>(sg, lp, lane) / (double)lp);
-  } else {
-    ms = int_mean_std<P>(v, lp, lane);
-  }
+  const MeanStd ms = ghist_meanstd<P, F>(g, lp, stage_all[wv]);
   if (lane == 0) {
     double* o = a.out + c * 22;
     o[4] = fabs(fx.xmax - fp.mu);          // s5 (:715)
@@ -498,6 +538,321 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     w->minbg = py_min(fp.mu, ms.mean);     // :724
     w->pstd = ms.std;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Pooled group-LM forms (lm_group.h) of the histogram fits, for histograms of <= 64 bins
+// (one 64-lane row in the wave layout, 4 rows per lane in a 16-lane group):
+//   k_ghistg  -- fitGaussian on the derivative histogram, then on the profile histogram,
+//                with the reference's retries (:949-978); each retry is a new fit in the slot
+//   k_gfixg   -- fitGaussianFixedWidthBins on the profile histogram, s5-s7
+// Candidates with wider histograms are marked ST_DEFER_HIST64 for k_ghist<.., D64>.
+// ---------------------------------------------------------------------------------------
+// the statistics fitGaussian starts from (:912-948): first argmax, its count, mean, std
+struct HStats {
+  int idx;
+  double a0, mean, s0;
+};
+__device__ __forceinline__ HStats hist_stats(const GaussFn<1>& fn, int nb) {
+  const int lane = lane_id();
+  const bool in = lane < nb;
+  const ArgMax am = wargmax(in ? fn.y[0] : -1.0, in ? lane : (1 << 30));
+  const double mean = wsum(in ? fn.y[0] : 0.0) / (double)nb;
+  const double d = in ? fn.y[0] - mean : 0.0;
+  const double s0 = sqrt(wsum(d * d) / (double)nb);
+  return {am.i, am.v, mean, s0};
+}
+
+template <int FPW>
+struct HistSlots {  // per slot and stage (0 = derivative, 1 = profile histogram)
+  double first[2][FPW], step[2][FPW], last[2][FPW];
+  int nb[2][FPW];
+};
+
+template <int P, bool F, int FPW>
+struct GhistProb {
+  BatesArgs a;
+  SlotTab<FPW>& T;    // pass = stage << 4 | retry
+  HistSlots<FPW>& HS;
+  double* cnt;        // wave scratch: counts [FPW][2][64]
+  int* hist;          // LDS [64]
+  double* sg;         // LDS stage (F)
+  int nslots;
+  __device__ __forceinline__ HistSpec spec(int st, int f) const {
+    HistSpec h;
+    h.first = HS.first[st][f];
+    h.step = HS.step[st][f];
+    h.last = HS.last[st][f];
+    h.nb = HS.nb[st][f];
+    return h;
+  }
+  // wave layout: the data rows of slot f's stage st (as load_hist + the zero padding)
+  __device__ __forceinline__ GaussFn<1> wave_rows(int st, int f) const {
+    GaussFn<1> fn;
+    const int lane = lane_id();
+    const HistSpec h = spec(st, f);
+    const int m = h.nb < 3 ? 3 : h.nb;
+    fn.ok[0] = lane < m;
+    fn.x[0] = lane < h.nb ? h.edge(lane) : 0.0;
+    fn.y[0] = lane < h.nb ? cnt[((size_t)f * 2 + st) * 64 + lane] : 0.0;
+    return fn;
+  }
+  __device__ __forceinline__ void start(int st, int f, BlmState<3, FPW>& S, int retry, double mu0) {
+    const GaussFn<1> fn = wave_rows(st, f);
+    const HStats hs = hist_stats(fn, HS.nb[st][f]);
+    const double mu = retry ? mu0 : bcast(fn.x[0], hs.idx);
+    if (lane_id() == 0) {
+      T.pass[f] = st << 4 | retry;
+      S.x[0][f] = hs.s0;
+      S.x[1][f] = mu;
+      S.x[2][f] = hs.a0;
+    }
+  }
+  __device__ __forceinline__ bool refill(int f, BlmState<3, FPW>& S) {
+    const int lane = lane_id();
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) {
+      const int st = T.pass[f] >> 4;
+      int retry = T.pass[f] & 15;
+      const int nb = HS.nb[st][f];
+      const int m = nb < 3 ? 3 : nb;
+      const GaussFn<1> fn = wave_rows(st, f);
+      const double p[3] = {S.x[0][f], S.x[1][f], S.x[2][f]};
+      const HStats hs = hist_stats(fn, nb);
+      // the retry rule of fitGaussian (:970-978), as fit_gaussian_hist
+      const double r = (lane < nb) ? fn.y[0] - fn.model(p, 0) : 0.0;
+      const double chisq = wsum(r * r) / (double)m;
+      bool fail = false, again = false;
+      double mu0 = 0.0;
+      if ((chisq > hs.mean * hs.mean * (double)nb) && (p[0] < 0.2 * (double)nb)) {
+        ++retry;
+        if (hs.idx + retry > nb) {
+          fail = true;
+        } else {
+          const bool in = lane < nb && (lane < hs.idx || lane >= hs.idx + retry);
+          const ArgMax t = wargmax(in ? fn.y[0] : -1.0, in ? lane : (1 << 30));
+          if (t.i >= (1 << 30)) {
+            fail = true;
+          } else {
+            const int pos = t.i < hs.idx ? t.i : t.i - retry;
+            if (pos + retry >= m) {
+              fail = true;
+            } else {
+              mu0 = bcast(fn.x[0], pos + retry);
+              again = retry <= 5;
+            }
+          }
+        }
+      }
+      if (again) {
+        start(st, f, S, retry, mu0);
+        blm_sync();
+        return true;
+      }
+      if (fail) {
+        if (lane == 0) a.status[c0] |= PFE_ST_GAUSS_FAIL;
+      } else if (st == 0) {
+        if (lane == 0) a.ws[c0].fd_mu = p[1];
+        start(1, f, S, 0, 0.0);
+        blm_sync();
+        return true;
+      } else {  // the profile-histogram fit: what k_gfixg and the later kernels need
+        GhPre<P, F> g;
+        ghist_prologue<P, F>(a, c0, g);  // (the profile rows again, for its mean / std)
+        const MeanStd ms = ghist_meanstd<P, F>(g, a.lp, sg);
+        if (lane == 0) {
+          GaussWS* w = a.ws + c0;
+          w->p_mu = p[1];
+          w->fp_amp = p[2];
+          w->minbg = py_min(p[1], ms.mean);  // :724
+          w->pstd = ms.std;
+        }
+      }
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_GHISTG);
+        if (c >= a.n) break;
+        GhPre<P, F> g;
+        ghist_prologue<P, F>(a, c, g);
+        uint32_t stt = 0;
+        if (g.nan || g.hb <= 0 || g.db <= 0 || g.hb < 2) stt = PFE_ST_GAUSS_FAIL;
+        else if (g.hb > 64 || g.db > 64) stt = ST_DEFER_HIST64;
+        if (stt) {
+          if (lane == 0) a.status[c] |= stt;
+          continue;
+        }
+        const HistSpec hd = hist_spec(g.dmin, g.dmax, g.db);
+        const HistSpec hp = hist_spec(g.vmin, g.vmax, g.hb);
+        double* cf = cnt + (size_t)f * 2 * 64;
+        build_hist<P>(hist, hd, g.d, g.okd);
+        cf[lane] = lane < hd.nb ? (double)hist[lane] : 0.0;
+        build_hist<P>(hist, hp, g.v, g.okv);
+        cf[64 + lane] = lane < hp.nb ? (double)hist[lane] : 0.0;
+        if (lane == 0) {
+          T.cand[f] = c;
+          HS.first[0][f] = hd.first;
+          HS.step[0][f] = hd.step;
+          HS.last[0][f] = hd.last;
+          HS.nb[0][f] = hd.nb;
+          HS.first[1][f] = hp.first;
+          HS.step[1][f] = hp.step;
+          HS.last[1][f] = hp.last;
+          HS.nb[1][f] = hp.nb;
+          GaussWS* w = a.ws + c;
+          w->h_min = g.vmin;
+          w->h_max = g.vmax;
+          w->hb = g.hb;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        blm_sync();
+        start(0, f, S, 0, 0.0);
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ GaussFn<4> load(int f) const {
+    GaussFn<4> fn;
+    const int gl = glane();
+    const int st = T.pass[f] >> 4;
+    const HistSpec h = spec(st, f);
+    const int m = h.nb < 3 ? 3 : h.nb;
+    const double* cf = cnt + ((size_t)f * 2 + st) * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = gl + GLM_G * k;
+      fn.ok[k] = i < m;
+      fn.x[k] = i < h.nb ? h.edge(i) : 0.0;
+      fn.y[k] = i < h.nb ? cf[i] : 0.0;
+    }
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 4; }
+};
+
+template <int P, bool F>
+__global__ __launch_bounds__(64, 2) void k_ghistg(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<3, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  __shared__ HistSlots<FPW> HS;
+  __shared__ int hist[64];
+  __shared__ double stage[F ? 64 * P : 1];
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
+  GhistProb<P, F, FPW> prob{a, T, HS, cnt, hist, stage, a.fpw};
+  glm_engine<3, 4, FPW>(prob, S, T.ph, T.list);
+}
+
+template <int P, bool F, int FPW>
+struct GfixProb {
+  BatesArgs a;
+  SlotTab<FPW>& T;  // d0 = first, d1 = step, d2 = last, mpad = nb of the profile histogram
+  double* cnt;      // wave scratch: counts [FPW][64]
+  int* hist;        // LDS [64]
+  int nslots;
+  __device__ __forceinline__ HistSpec spec(int f) const {
+    HistSpec h;
+    h.first = T.d0[f];
+    h.step = T.d1[f];
+    h.last = T.d2[f];
+    h.nb = T.mpad[f];
+    return h;
+  }
+  __device__ __forceinline__ double xmax_of(const HistSpec& h) const {
+    int xi = h.nb / 2 - 1;  // xData[int(bins/2)-1] (index -1 = last bin) (:1041)
+    if (xi < 0) xi += h.nb;
+    return h.edge(xi);
+  }
+  __device__ __forceinline__ bool refill(int f, BlmState<2, FPW>& S) {
+    const int lane = lane_id();
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0 && lane == 0) {
+      const GaussWS* w = a.ws + c0;
+      const double xmax = xmax_of(spec(f));
+      double* o = a.out + c0 * 22;
+      o[4] = fabs(xmax - w->p_mu);         // s5 (:715)
+      o[5] = fabs(S.x[1][f] / w->fp_amp);  // s6 (:716)
+      o[6] = fabs(w->fd_mu - w->p_mu);     // s7 (:717)
+    }
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_GFIXG);
+        if (c >= a.n) break;
+        if (a.status[c] & (PFE_ST_GAUSS_FAIL | ST_DEFER_HIST64)) continue;
+        const GaussWS* w = a.ws + c;
+        const HistSpec hp = hist_spec(w->h_min, w->h_max, w->hb);
+        GhPre<P, F> g;  // the profile rows (the bin counts are not needed again)
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const int i = lane + 64 * k;
+          g.okv[k] = i < a.lp;
+          if constexpr (F)
+            g.v[k] = g.okv[k] ? a.fprof[c * a.lp + i] : 0.0;
+          else
+            g.v[k] = g.okv[k] ? (int)a.prof[c * a.lp + i] : 0;
+        }
+        build_hist<P>(hist, hp, g.v, g.okv);
+        const bool in = lane < hp.nb;
+        const double y = in ? (double)hist[lane] : 0.0;
+        cnt[(size_t)f * 64 + lane] = y;
+        // start point (:1034-1045): std of the counts, their maximum
+        const double cmax = wmax(in ? y : -1.0);
+        const double mean = wsum(y) / (double)hp.nb;
+        const double d = in ? y - mean : 0.0;
+        const double s0 = sqrt(wsum(d * d) / (double)hp.nb);
+        if (lane == 0) {
+          T.cand[f] = c;
+          T.d0[f] = hp.first;
+          T.d1[f] = hp.step;
+          T.d2[f] = hp.last;
+          T.mpad[f] = hp.nb;
+          S.x[0][f] = s0;
+          S.x[1][f] = cmax;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ GaussFixedFn<4> load(int f) const {
+    GaussFixedFn<4> fn;
+    const int gl = glane();
+    const HistSpec h = spec(f);
+    const double* cf = cnt + (size_t)f * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = gl + GLM_G * k;
+      fn.ok[k] = i < h.nb;
+      fn.x[k] = i < h.nb ? h.edge(i) : 0.0;
+      fn.y[k] = i < h.nb ? cf[i] : 0.0;
+    }
+    fn.xmax = xmax_of(h);
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 3; }
+};
+
+template <int P, bool F>
+__global__ __launch_bounds__(64, 2) void k_gfixg(BatesArgs a) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<2, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  __shared__ int hist[64];
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
+  GfixProb<P, F, FPW> prob{a, T, cnt, hist, a.fpw};
+  glm_engine<2, 4, FPW>(prob, S, T.ph, T.list);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1596,7 +1951,17 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const dim3 pool((unsigned)a.pwaves);
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
-    if (a.fprof) {                                                                      \
+    if (use_glm && a.fprof) {                                                           \
+      hipLaunchKernelGGL((k_ghistg<(P <= 2 ? P : 2), true>), pool, dim3(64), 0, st, a); \
+      hipLaunchKernelGGL((k_gfixg<(P <= 2 ? P : 2), true>), pool, dim3(64), 0, st, a);  \
+      hipLaunchKernelGGL((k_ghist<P, 4, false, true, true>), gw(a.n), dim3(BLOCK), 0, st, a); \
+      hipLaunchKernelGGL((k_ghist<P, 16, true, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
+    } else if (use_glm) {                                                               \
+      hipLaunchKernelGGL((k_ghistg<(P <= 2 ? P : 2), false>), pool, dim3(64), 0, st, a); \
+      hipLaunchKernelGGL((k_gfixg<(P <= 2 ? P : 2), false>), pool, dim3(64), 0, st, a);  \
+      hipLaunchKernelGGL((k_ghist<P, 4, false, false, true>), gw(a.n), dim3(BLOCK), 0, st, a); \
+      hipLaunchKernelGGL((k_ghist<P, 16, true, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
+    } else if (a.fprof) {                                                               \
       hipLaunchKernelGGL((k_ghist<P, 4, false, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
       hipLaunchKernelGGL((k_ghist<P, 16, true, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
     } else {                                                                            \
