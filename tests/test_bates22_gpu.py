@@ -153,3 +153,34 @@ def test_pooled_group_solver(engine, monkeypatch, lp):
     o2, s2 = engine.bates22(b["prof"][perm], b["sub"][perm], b["dmcurve"][perm], b["scal"][perm])
     assert np.array_equal(s2, s1[perm])
     assert np.array_equal(np.nan_to_num(o2, nan=7.0), np.nan_to_num(o1[perm], nan=7.0))
+
+
+def wide_histogram_batch(n, seed):
+    """Profiles with low noise under a strong narrow pulse: Freedman-Diaconis bin counts of
+    ~40 (pooled kernels), ~100-190 (deferred to the wave kernel, > 64 bins) and ~350-390
+    (the wide-histogram kernel, > 256 bins)."""
+    b = bates_batch(n, seed=seed)
+    rng = np.random.default_rng(seed)
+    lp = b["prof"].shape[1]
+    x = np.arange(lp)
+    prof = np.empty((n, lp))
+    for i in range(n):
+        kind = i % 3
+        sd = (2.5, 0.7, 6.0)[kind]
+        base = rng.normal(100 if kind != 1 else 50, sd, lp)
+        mu, w = rng.uniform(10, lp - 10), rng.uniform(1.0, 3.0)
+        prof[i] = base + 150 * np.exp(-0.5 * ((x - mu) / w) ** 2)
+    b["prof"] = np.clip(np.rint(prof), 0, 255).astype(np.uint8)
+    return b
+
+
+def test_wide_histograms_vs_oracle(engine):
+    """Every histogram-width class in one batch: the pooled kernels take <= 64 bins and pass
+    wider ones on (ST_DEFER_HIST64, ST_DEFER_HIST); all of them against the oracle."""
+    b = wide_histogram_batch(60, 5)
+    out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert not (st & 0xFFFF0000).any(), "internal deferral bits left in status"
+    ref, rst, own = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    gold = FLOOR["bates22_phcx128"]
+    floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
+    check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor)
