@@ -5,6 +5,7 @@
 //   k_sine (s1-s4) -> k_ghist (+ k_ghist<BIG> for wide histograms) -> k_gt1 (s8,s9)
 //   -> k_gdg (s10,s11) -> k_dmfit (s12-s19) -> k_subband (s20-s22)
 #include <cmath>
+#include <cstdlib>
 
 #include "bates_common.h"
 
@@ -33,8 +34,18 @@ static int blm_fits_per_wave(int64_t n, int cus) {
   return (int)(f < 4 ? 4 : f > BLM_FPW ? BLM_FPW : f);
 }
 
-// persistent waves of the batched kernels: enough to fill every CU (8 waves each), never
-// more than there are batches
+// Fit slots per wave of the pooled kernels (lm_group.h): a wave works its slots in groups of
+// 4 and runs lmpar one slot per lane, so it wants many; but n / slots waves should still
+// cover the chip's wave slots (CUs x 8) -- PFE_GSLOTS overrides (A/B runs)
+static int glm_slots(int64_t n, int cus) {
+  const char* e = getenv("PFE_GSLOTS");
+  if (e && atoi(e) > 0) return atoi(e) > GLM_FPW ? GLM_FPW : atoi(e);
+  const int64_t f = n / ((int64_t)cus * 8);
+  return (int)(f < 4 ? 4 : f > GLM_FPW ? GLM_FPW : f);
+}
+
+// persistent waves of the batched and pooled kernels: enough to fill every CU (8 waves
+// each), never more than there are batches
 static int persistent_waves(int64_t n) {
   const int cus = device_cus();
   const int fpw = blm_fits_per_wave(n, cus);
@@ -73,6 +84,7 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());
+  a.gslots = glm_slots(n, device_cus());
   a.lp = lp;
   a.n = n;
   // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code

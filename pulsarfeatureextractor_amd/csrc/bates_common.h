@@ -53,6 +53,7 @@ struct BatesArgs {
   int pwaves;          // number of persistent waves wscr is sized for
   int fpw;             // fits per wave of the batched kernels (<= BLM_FPW): small batches
                        // use fewer so that there are several waves per wave slot
+  int gslots;          // fit slots per wave of the pooled kernels (<= GLM_FPW)
 };
 
 constexpr int BATES_NCOUNTERS = 16;

@@ -745,7 +745,7 @@ __global__ __launch_bounds__(64, 2) void k_ghistg(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
-  GhistProb<P, F, FPW> prob{a, T, HS, cnt, hist, stage, a.fpw};
+  GhistProb<P, F, FPW> prob{a, T, HS, cnt, hist, stage, a.gslots};
   glm_engine<3, 4, FPW>(prob, S, T.ph, T.list);
 }
 
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(64, 2) void k_gfixg(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
-  GfixProb<P, F, FPW> prob{a, T, cnt, hist, a.fpw};
+  GfixProb<P, F, FPW> prob{a, T, cnt, hist, a.gslots};
   glm_engine<2, 4, FPW>(prob, S, T.ph, T.list);
 }
 
@@ -1745,7 +1745,7 @@ __global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gt1Prob<P, FPW> prob{a, T, a.fpw};
+  Gt1Prob<P, FPW> prob{a, T, a.gslots};
   glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
 }
 
@@ -1868,7 +1868,7 @@ __global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
   blm_sync();
   double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   double* yv = xs + (size_t)FPW * 64 * P;
-  PeelProb<P, FPW> prob{a, T, xs, yv, ys, cx, a.fpw};
+  PeelProb<P, FPW> prob{a, T, xs, yv, ys, cx, a.gslots};
   glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
 }
 
@@ -1933,7 +1933,7 @@ __global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gdg8Prob<P, FPW> prob{a, T, a.fpw};
+  Gdg8Prob<P, FPW> prob{a, T, a.gslots};
   glm_engine<8, 4 * P, FPW>(prob, S, T.ph, T.list);
 }
 

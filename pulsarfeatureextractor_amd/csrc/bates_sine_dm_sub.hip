@@ -379,7 +379,7 @@ __global__ __launch_bounds__(64, 2) void k_sineg(BatesArgs a) {
   __shared__ double stage[F ? 64 * MPL : 1];
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  SineProb<MPL, F, FPW> prob{a, T, stage, a.fpw};
+  SineProb<MPL, F, FPW> prob{a, T, stage, a.gslots};
   glm_engine<2, 4 * MPL, FPW>(prob, S, T.ph, T.list);
 }
 
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(64, 2) void k_dmfitg(BatesArgs a) {
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  DMProb<MPL, FPW> prob{a, T, a.fpw};
+  DMProb<MPL, FPW> prob{a, T, a.gslots};
   glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list);
 }
 

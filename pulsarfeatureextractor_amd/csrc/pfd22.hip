@@ -12,6 +12,7 @@
 
 #include "bates_common.h"
 #include "lm_batch.h"
+#include "lm_group.h"
 #include "pfd.h"
 
 namespace pfe {
@@ -57,15 +58,21 @@ struct PfdDMArgs {
 
 // the fit data of candidate c (:322-352): yData = 255./max(chis)*chis in float32 (numpy's
 // scalar rules, as the reference runs under the numpy this build is pinned against)
-template <int MPL>
-__device__ __forceinline__ void pfd_dm_functor(const PfdDMArgs& d, int64_t c, PfdDMFn<MPL>& fn) {
-  const int lane = lane_id();
-  const double* q = d.a.scal + c * 8;
+__device__ __forceinline__ float pfd_dm_scale(const PfdDMArgs& d, int64_t c) {
   const float* ch = d.chis + c * PFE_PFD_NDM;
   float m = ch[0];  // Python max() over the float32 array
   for (int i = 1; i < PFE_PFD_NDM; ++i)
     if (ch[i] > m) m = ch[i];
-  const float s = 255.0f / m;
+  return 255.0f / m;
+}
+
+// rows i = lb + STRIDE*k: the wave layout (lane, 64) or the group layout (glane, 16); s is
+// pfd_dm_scale(d, c)
+template <int MPL, int STRIDE = 64>
+__device__ __forceinline__ void pfd_dm_functor(const PfdDMArgs& d, int64_t c, PfdDMFn<MPL>& fn,
+                                               float s, int lb = lane_id()) {
+  const double* q = d.a.scal + c * 8;
+  const float* ch = d.chis + c * PFE_PFD_NDM;
   const double dm_start = q[4], dm_end = q[5];
   const double step = fabs(dm_start - dm_end) / (double)PFE_PFD_NDM;   // :338
   fn.period = q[0];
@@ -73,7 +80,7 @@ __device__ __forceinline__ void pfd_dm_functor(const PfdDMArgs& d, int64_t c, Pf
   fn.wint = (q[3] * q[0]) * (q[3] * q[0]);                              // :341
 #pragma unroll
   for (int k = 0; k < MPL; ++k) {
-    const int i = lane + 64 * k;
+    const int i = lb + STRIDE * k;
     fn.ok[k] = i < PFE_PFD_NDM;
     fn.y[k] = fn.ok[k] ? (double)(s * ch[fn.ok[k] ? i : 0]) : 0.0;
     fn.x[k] = dm_start + (double)i * step;                              // :349-352
@@ -110,7 +117,7 @@ struct PfdDMLoader {
   int64_t base;
   __device__ __forceinline__ PfdDMFn<MPL> operator()(int f) const {
     PfdDMFn<MPL> fn;
-    pfd_dm_functor<MPL>(d, base + f, fn);
+    pfd_dm_functor<MPL>(d, base + f, fn, pfd_dm_scale(d, base + f));
     return fn;
   }
 };
@@ -138,7 +145,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
   for (uint64_t m = fits; m; m &= m - 1) {
     const int f = __builtin_ctzll(m);
     PfdDMFn<MPL> fn;
-    pfd_dm_functor<MPL>(d, base + f, fn);
+    pfd_dm_functor<MPL>(d, base + f, fn, pfd_dm_scale(d, base + f));
     double theo[MPL], amp0 = 0.0;
     if (!pfd_dm_theo<MPL>(fn, theo, amp0)) {  // ZeroDivisionError
       if (lane == 0) a.status[base + f] |= PFE_ST_DMFIT_FAIL;
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
     const int f = __builtin_ctzll(m);
     const int64_t c = base + f;
     PfdDMFn<MPL> fn;
-    pfd_dm_functor<MPL>(d, c, fn);
+    pfd_dm_functor<MPL>(d, c, fn, pfd_dm_scale(d, c));
     double theo[MPL], amp0 = 0.0;
     pfd_dm_theo<MPL>(fn, theo, amp0);
 #pragma unroll
@@ -194,6 +201,118 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// s16-s19 of candidate c after the fit (whole wave): chi^2 of the theoretical curve over
+// the bins where it is > 0, a Python loop (sequential, lane 0 over LDS terms)
+template <int MPL>
+__device__ __forceinline__ void pfd_dm_finish(const PfdDMArgs& d, int64_t c, double prop,
+                                              double shift, double* term, int* used) {
+  const BatesArgs& a = d.a;
+  const int lane = lane_id();
+  PfdDMFn<MPL> fn;
+  pfd_dm_functor<MPL>(d, c, fn, pfd_dm_scale(d, c));
+  double theo[MPL], amp0 = 0.0;
+  pfd_dm_theo<MPL>(fn, theo, amp0);
+#pragma unroll
+  for (int k = 0; k < MPL; ++k) {
+    const int i = lane + 64 * k;
+    if (fn.ok[k]) {
+      const double dd = fn.y[k] - theo[k];
+      used[i] = theo[k] > 0.0;                                        // :381
+      term[i] = (dd * dd) / theo[k];                                  // :383
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    const double* q = a.scal + c * 8;
+    const double period = q[0], snr = q[1];
+    const double wint = fn.wint;
+    double chi = 0.0;
+    int ndeg = 0;
+    for (int i = 0; i < PFE_PFD_NDM; ++i)
+      if (used[i]) {
+        chi += term[i];
+        ++ndeg;
+      }
+    double* o = a.out + c * 22;
+    o[15] = snr / sqrt((period - sqrt(wint)) / sqrt(wint));          // s16 (:346)
+    o[16] = fabs(1.0 - prop);                                        // s17 (:391)
+    o[17] = fabs(shift);                                             // s18, filterScore(18)
+    o[18] = ndeg ? chi / (double)ndeg : 0.0;                         // s19 (:387)
+    if (!ndeg) a.status[c] |= PFE_ST_DMFIT_FAIL;                     // ZeroDivisionError
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// pooled group-LM form (lm_group.h) of the clamped 4-parameter DM fit
+template <int MPL, int FPW>
+struct PfdDMProb {
+  static constexpr int MG = 4 * MPL;
+  PfdDMArgs d;
+  SlotTab<FPW>& T;  // d0 = 255/max(chis) of the slot's candidate
+  double* term;
+  int* used;
+  int nslots;
+  __device__ __forceinline__ bool refill(int f, BlmState<4, FPW>& S) {
+    const BatesArgs& a = d.a;
+    const int lane = lane_id();
+    const int64_t c0 = T.cand[f];
+    if (c0 >= 0) pfd_dm_finish<MPL>(d, c0, S.x[1][f], S.x[2][f], term, used);
+    if (f < nslots) {
+      for (;;) {
+        const int64_t c = queue_next(a.counters + CTR_PFDDMG);
+        if (c >= a.n) break;
+        const uint32_t st = a.status[c];
+        if (st & PFE_ST_PFD_DMCURVE_FAIL) {  // numdms == 1: dms[0] raises in getDMFittings
+          if (lane == 0) a.status[c] = (st & ~PFE_ST_PFD_DMCURVE_FAIL) | PFE_ST_DMFIT_FAIL;
+          continue;
+        }
+        const float sc = pfd_dm_scale(d, c);
+        PfdDMFn<MPL> fn;
+        pfd_dm_functor<MPL>(d, c, fn, sc);
+        double theo[MPL], amp0 = 0.0;
+        if (!pfd_dm_theo<MPL>(fn, theo, amp0)) {  // ZeroDivisionError
+          if (lane == 0) a.status[c] |= PFE_ST_DMFIT_FAIL;
+          continue;
+        }
+        if (lane == 0) {
+          T.cand[f] = c;
+          T.d0[f] = (double)sc;
+          S.x[0][f] = amp0;
+          S.x[1][f] = 1.0;
+          S.x[2][f] = 0.0;
+          S.x[3][f] = 0.0;
+        }
+        blm_sync();
+        return true;
+      }
+    }
+    if (lane == 0) T.cand[f] = -1;
+    blm_sync();
+    return false;
+  }
+  __device__ __forceinline__ PfdDMFn<MG> load(int f) const {
+    PfdDMFn<MG> fn;
+    pfd_dm_functor<MG, GLM_G>(d, T.cand[f], fn, (float)T.d0[f], glane());
+    return fn;
+  }
+  __device__ __forceinline__ int maxfev(int) const { return 200 * 5; }
+};
+
+template <int MPL>
+__global__ __launch_bounds__(64, 2) void k_pfd_dmfitg(PfdDMArgs d) {
+  constexpr int FPW = GLM_FPW;
+  __shared__ BlmState<4, FPW> S;
+  __shared__ SlotTab<FPW> T;
+  __shared__ double term[64 * MPL];
+  __shared__ int used[64 * MPL];
+  if (lane_id() < FPW) T.cand[lane_id()] = -1;
+  blm_sync();
+  PfdDMProb<MPL, FPW> prob{d, T, term, used, d.a.gslots};
+  glm_engine<4, 4 * MPL, FPW>(prob, S, T.ph, T.list);
 }
 
 size_t pfd22_workspace_bytes(int64_t n, int L) {
@@ -249,8 +368,13 @@ hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, s
   if ((e = launch_sine(a, st)) != hipSuccess) return e;
   if ((e = launch_gauss(a, st)) != hipSuccess) return e;
   const PfdDMArgs d{a, chis};
-  hipLaunchKernelGGL((k_pfd_dmfitb<2, BLM_FPW>), dim3((unsigned)((n + a.fpw - 1) / a.fpw)),
-                     dim3(64), 0, st, d);
+  const char* g = getenv("PFE_GLM");
+  const char* b = getenv("PFE_BLM");
+  if (!(g && g[0] == '0') && !(b && b[0] == '0'))  // pooled group-LM unless an A/B run opts out
+    hipLaunchKernelGGL((k_pfd_dmfitg<2>), dim3((unsigned)a.pwaves), dim3(64), 0, st, d);
+  else
+    hipLaunchKernelGGL((k_pfd_dmfitb<2, BLM_FPW>), dim3((unsigned)((n + a.fpw - 1) / a.fpw)),
+                       dim3(64), 0, st, d);
   launch_clear_internal(status, n, st);
   return hipGetLastError();
 }
