@@ -12,6 +12,7 @@
 // split at n/2 rounded down to a multiple of 8), and the DM-curve statistics run in float32
 // as numpy does on a float32 array.  The sub-band profiles of the candidate live in LDS.
 #include <cmath>
+#include <cstdlib>
 
 #include "np_sum.h"
 #include "pfd.h"
@@ -317,6 +318,61 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   return true;
 }
 
+// the rest of a fold after the chi^2 sweep (one wave): DM-curve statistics, the 22-score
+// parameters and sub-band scores, status
+__device__ __forceinline__ void pfd_finish(const PfdArgs& a, int64_t c, double* T, double* buf,
+                                        double* tmp, double* dl, double* sdb, double* bv,
+                                        float* chs, float* ftmp, const double (&po)[4],
+                                        bool dm_ok, int lane) {
+  const double* sc = a.scal + c * PFE_PFD_NSCAL;
+  const double bestdm = sc[PFE_PFD_BESTDM];
+  const double dm_lo = sc[PFE_PFD_DM_LO], dm_hi = sc[PFE_PFD_DM_HI];
+  const int NS = a.nsub, L = a.L;
+  if (a.lyon8) {
+    double dmo[4] = {0.0, 0.0, 0.0, 0.0};
+    if (dm_ok) stats4_f32(chs, ftmp, PFE_PFD_NDM, dmo);
+    if (lane == 0) {
+      double* o = a.lyon8 + c * 8;
+      for (int i = 0; i < 4; ++i) {
+        o[i] = po[i];
+        o[4 + i] = dm_ok ? dmo[i] : NAN;
+      }
+    }
+  }
+  uint32_t st = dm_ok ? 0u : PFE_ST_PFD_DMCURVE_FAIL;
+  if (a.out22) {
+    double snr, width;
+    pfd_params(buf, tmp, L, lane, snr, width);
+    const double period = sc[PFE_PFD_BARY_P1] * 1000.0;            // PFDOperations.py:127
+    const double span1 = dm_lo + ((dm_hi - dm_lo) * 1.0) / (double)(PFE_PFD_NDM - 1);
+    const double span_last =
+        dm_lo + ((dm_hi - dm_lo) * (double)(PFE_PFD_NDM - 1)) / (double)(PFE_PFD_NDM - 1);
+    double sb[3];
+    const bool sb_ok = pfd_subband_scores(T, buf, tmp, dl, sdb, bv, NS, L, lane, width, sb);
+    if (!sb_ok) st |= PFE_ST_SUBBAND_FAIL;
+    if (lane == 0) {
+      double* o = a.out22 + c * 22;
+      o[11] = period;                                                 // s12 (PFDFile.py:776)
+      o[12] = filter_neg_pfd(snr);                                    // s13 (:777)
+      o[13] = filter_neg_pfd(bestdm);                                 // s14 (:778)
+      o[14] = width;                                                  // s15
+      o[19] = sb[0];                                                  // s20 (:861-863)
+      o[20] = sb[1];                                                  // s21
+      o[21] = sb[2];                                                  // s22
+      double* q = a.par22 + c * 8;
+      q[0] = period;
+      q[1] = snr;
+      q[2] = bestdm;
+      q[3] = width;
+      q[4] = span1;      // float(dm_index[1])            (PFDOperations.py:337)
+      q[5] = span_last;  // float(dm_index[len - 1])
+      q[6] = 0.0;
+      q[7] = 0.0;
+    }
+  }
+  if (lane == 0) a.status[c] = st;
+}
+
 __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   extern __shared__ double lds[];
   const int64_t c = blockIdx.x;
@@ -424,49 +480,181 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
     }
     lds_sync();
   }
-  if (a.lyon8) {
-    double dmo[4] = {0.0, 0.0, 0.0, 0.0};
-    if (dm_ok) stats4_f32(chs, ftmp, PFE_PFD_NDM, dmo);
-    if (lane == 0) {
-      double* o = a.lyon8 + c * 8;
-      for (int i = 0; i < 4; ++i) {
-        o[i] = po[i];
-        o[4 + i] = dm_ok ? dmo[i] : NAN;
+  pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
+}
+
+// Four-wave form of k_pfd_dmprof for profiles of <= 128 bins (the same arithmetic, bit for
+// bit).  The single-wave kernel streamed the fold with one dependent load per lane at a time
+// and swept the 100 trial DMs one after another; here
+//   * all 256 threads reduce the fold over its parts, 4 elements x 4 parts of independent
+//     loads in flight per thread (each element still sums its parts in order, as numpy);
+//   * wave 1 tabulates the accumulated sub-band rotations of all 100 trial DMs;
+//   * the sweep runs 32 trial DMs at a time, 8 lanes per DM: lane a accumulates numpy's
+//     pairwise-leaf partial r_a = x_a + x_{a+8} + ... of the DM's chi^2 terms directly from
+//     the sub-band rows in LDS, and the 8 partials combine in numpy's order;
+//   * wave 0 builds the profile and finishes the fold (statistics, 22-score parameters) as
+//     the single-wave kernel.
+__global__ __launch_bounds__(256) void k_pfd_dmprof4(PfdArgs a) {
+  extern __shared__ double lds[];
+  const int64_t c = blockIdx.x;
+  if (c >= a.n) return;
+  const int tid = threadIdx.x;
+  const int wv = tid >> 6;
+  const int lane = lane_id();
+  const int NP = a.npart, NS = a.nsub, L = a.L;
+  double* T = lds;                   // NS x L
+  double* buf = T + (size_t)NS * L;  // L
+  double* tmp = buf + L;             // L
+  double* dl = tmp + L;              // NS
+  double* sdb = dl + NS;             // NS
+  double* bv = sdb + NS;             // NS
+  int* cum = (int*)(bv + NS);        // NS
+  int* rot = cum + NS;               // PFE_PFD_NDM x NS accumulated rotations of the sweep
+  __shared__ float chs[PFE_PFD_NDM], ftmp[PFE_PFD_NDM];
+  const double* sc = a.scal + c * PFE_PFD_NSCAL;
+  const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
+  const double avgprof = sc[PFE_PFD_AVGPROF], varprof = sc[PFE_PFD_VARPROF];
+  const double dm_lo = sc[PFE_PFD_DM_LO], dm_hi = sc[PFE_PFD_DM_HI];
+  const double numdms = sc[PFE_PFD_NUMDMS];
+  const double* fr = a.subfreqs + c * NS;
+  const double* P = a.profs + c * (int64_t)NP * NS * L;
+  const bool dm_ok = numdms > 1.0;  // numdms == 1: dms is a scalar and dms[0] raises
+  const bool sweep = dm_ok && (a.chis || a.lyon8);
+  // ---- dedisperse at the best DM (PFDFile.py:346-373, interp = 0)
+  if (wv == 0) {
+    for (int j = lane; j < NS; j += 64) dl[j] = delay_from_dm(bestdm, fr[j]);
+    lds_sync();
+    const double hif = dl[NS - 1];
+    for (int j = lane; j < NS; j += 64) {
+      const double delaybins = (dl[j] - hif) * bps - 0.0;
+      const double nw = floor(delaybins + 0.5);
+      sdb[j] = 0.0 + nw;
+      cum[j] = pymod((long long)nw, L);
+    }
+  }
+  __syncthreads();
+  // T[j][b] = sum over parts of the rotated sub-integration profiles (profs.sum(0))
+  {
+    const int total = NS * L;
+    const int64_t pstride = (int64_t)NS * L;
+    for (int e0 = tid; e0 < total; e0 += 256 * 4) {
+      int src[4];
+      bool ok[4];
+      double acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u;
+        ok[u] = e < total;
+        const int j = ok[u] ? e / L : 0;
+        const int b = ok[u] ? e - j * L : 0;
+        const int r = cum[j];
+        src[u] = j * L + (b + r < L ? b + r : b + r - L);
+        acc[u] = ok[u] ? P[src[u]] : 0.0;
+      }
+#pragma unroll 4
+      for (int p = 1; p < NP; ++p) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ok[u] ? P[p * pstride + src[u]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += v[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) T[e0 + 256 * u] = acc[u];
+    }
+  }
+  __syncthreads();
+  if (wv == 1 && sweep) {
+    // the sweep's accumulated rotations (PFDFile.py:395-416): each lane follows its sub-bands
+    // through the 100 trial DMs
+    for (int j = lane; j < NS; j += 64) {
+      int cu = 0;
+      double sd = sdb[j];
+      for (int k = 0; k < PFE_PFD_NDM; ++k) {
+        const double dm = dm_lo + ((dm_hi - dm_lo) * (double)k) / (double)(PFE_PFD_NDM - 1);
+        const double hif = delay_from_dm(dm, fr[NS - 1]);
+        const double delaybins = (delay_from_dm(dm, fr[j]) - hif) * bps - sd;
+        const double nw = floor(delaybins + 0.5);
+        cu = pymod((long long)cu + (long long)nw, L);
+        sd = sd + nw;
+        rot[k * NS + j] = cu;
       }
     }
   }
-  uint32_t st = dm_ok ? 0u : PFE_ST_PFD_DMCURVE_FAIL;
-  if (a.out22) {
-    double snr, width;
-    pfd_params(buf, tmp, L, lane, snr, width);
-    const double period = sc[PFE_PFD_BARY_P1] * 1000.0;            // PFDOperations.py:127
-    const double span1 = dm_lo + ((dm_hi - dm_lo) * 1.0) / (double)(PFE_PFD_NDM - 1);
-    const double span_last =
-        dm_lo + ((dm_hi - dm_lo) * (double)(PFE_PFD_NDM - 1)) / (double)(PFE_PFD_NDM - 1);
-    double sb[3];
-    const bool sb_ok = pfd_subband_scores(T, buf, tmp, dl, sdb, bv, NS, L, lane, width, sb);
-    if (!sb_ok) st |= PFE_ST_SUBBAND_FAIL;
-    if (lane == 0) {
-      double* o = a.out22 + c * 22;
-      o[11] = period;                                                 // s12 (PFDFile.py:776)
-      o[12] = filter_neg_pfd(snr);                                    // s13 (:777)
-      o[13] = filter_neg_pfd(bestdm);                                 // s14 (:778)
-      o[14] = width;                                                  // s15
-      o[19] = sb[0];                                                  // s20 (:861-863)
-      o[20] = sb[1];                                                  // s21
-      o[21] = sb[2];                                                  // s22
-      double* q = a.par22 + c * 8;
-      q[0] = period;
-      q[1] = snr;
-      q[2] = bestdm;
-      q[3] = width;
-      q[4] = span1;      // float(dm_index[1])            (PFDOperations.py:337)
-      q[5] = span_last;  // float(dm_index[len - 1])
-      q[6] = 0.0;
-      q[7] = 0.0;
+  __syncthreads();
+  // ---- chi^2 versus DM over span(dms[0], dms[-1], 100) (PFDFile.py:378-423)
+  if (sweep) {
+    const int g = tid >> 3, ai = tid & 7;
+    const int nb = L - (L % 8);
+    for (int k = g; k < PFE_PFD_NDM; k += 256 / 8) {
+      const int* rk = rot + k * NS;
+      auto xval = [&](int b) {
+        double s = 0.0;
+        for (int j = 0; j < NS; ++j) {
+          int src = b + rk[j];
+          if (src >= L) src -= L;
+          const double v = T[(size_t)j * L + src];
+          s = (j == 0) ? v : s + v;
+        }
+        const double d = s - avgprof;
+        return (d * d) / varprof;
+      };
+      double res;
+      if (L < 8) {  // np_leaf, n < 8
+        res = 0.0;
+        if (ai == 0)
+          for (int i = 0; i < L; ++i) res += xval(i);
+      } else {
+        double r = xval(ai);
+        for (int b = 8 + ai; b < nb; b += 8) r += xval(b);
+        const int base = lane & ~7;
+        const double r0 = __shfl(r, base + 0), r1 = __shfl(r, base + 1);
+        const double r2 = __shfl(r, base + 2), r3 = __shfl(r, base + 3);
+        const double r4 = __shfl(r, base + 4), r5 = __shfl(r, base + 5);
+        const double r6 = __shfl(r, base + 6), r7 = __shfl(r, base + 7);
+        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        if (ai == 0)
+          for (int i = nb; i < L; ++i) res += xval(i);
+      }
+      if (ai == 0) {
+        const float chi = (float)(res / ((double)L - 1.0));
+        chs[k] = chi;
+        if (a.chis) a.chis[c * PFE_PFD_NDM + k] = chi;
+      }
     }
   }
-  if (lane == 0) a.status[c] = st;
+  __syncthreads();
+  if (wv != 0) return;
+  // (the profile is built after the sweep: it does not feed it, and the wave-0-only calls it
+  // makes kept out of the divergent part before the sweep)
+  double po[4] = {0.0, 0.0, 0.0, 0.0};
+  {
+    // sumprof = T.sum(0); the profile (getprofile + scale)
+    for (int b = lane; b < L; b += 64) {
+      double s = T[b];
+      for (int j = 1; j < NS; ++j) s += T[(size_t)j * L + b];
+      buf[b] = s;
+    }
+    lds_sync();
+    const double mn = py_min_seq(buf, L);
+    for (int b = lane; b < L; b += 64) buf[b] = buf[b] - mn;  // normprof
+    lds_sync();
+    const double mean = np_pairwise<12>(buf, L, lane) / (double)L;
+    lds_sync();
+    for (int b = lane; b < L; b += 64) buf[b] = buf[b] / mean;  // s
+    lds_sync();
+    const double smin = py_min_seq(buf, L), smax = py_max_seq(buf, L);
+    lds_sync();
+    for (int b = lane; b < L; b += 64) {
+      const double t = (buf[b] - smin) / (smax - smin);
+      buf[b] = (0.0 * (1.0 - t)) + (255.0 * t);
+      if (a.profile) a.profile[c * L + b] = buf[b];
+    }
+    lds_sync();
+    if (a.lyon8) stats4_f64(buf, tmp, L, lane, po);
+  }
+  pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
 size_t pfd_lds_bytes(int nsub, int L) {
@@ -474,7 +662,24 @@ size_t pfd_lds_bytes(int nsub, int L) {
          (size_t)nsub * sizeof(int) + 64;
 }
 
+static size_t pfd4_lds_bytes(int nsub, int L) {
+  return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int);
+}
+
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {
+  const char* e4 = getenv("PFE_PFD4");
+  if (a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && !(e4 && e4[0] == '0')) {
+    const size_t lds4 = pfd4_lds_bytes(a.nsub, a.L);
+    static size_t configured4 = 0;
+    if (lds4 > 48 * 1024 && lds4 > configured4) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_pfd_dmprof4,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);
+      if (e != hipSuccess) return e;
+      configured4 = lds4;
+    }
+    hipLaunchKernelGGL(k_pfd_dmprof4, dim3((unsigned)a.n), dim3(256), lds4, st, a);
+    return hipGetLastError();
+  }
   const size_t lds = pfd_lds_bytes(a.nsub, a.L);
   static size_t configured = 0;
   if (lds > 48 * 1024 && lds > configured) {
