@@ -483,18 +483,41 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
+constexpr int PFD4_E = 8;  // fold elements per thread and load step of k_pfd_dmprof4
+
+// the accumulated sub-band rotations of the 100 trial DMs (PFDFile.py:395-416), one lane
+// per sub-band: rot[k][j] (the sweep of the single-wave kernel keeps them in cum / sdb)
+__device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, const double* fr,
+                                                int NS, int L, double bps, double dm_lo,
+                                                double dm_hi, int lane) {
+  for (int j = lane; j < NS; j += 64) {
+    int cu = 0;
+    double sd = sdb[j];
+    for (int k = 0; k < PFE_PFD_NDM; ++k) {
+      const double dm = dm_lo + ((dm_hi - dm_lo) * (double)k) / (double)(PFE_PFD_NDM - 1);
+      const double hif = delay_from_dm(dm, fr[NS - 1]);
+      const double delaybins = (delay_from_dm(dm, fr[j]) - hif) * bps - sd;
+      const double nw = floor(delaybins + 0.5);
+      cu = pymod((long long)cu + (long long)nw, L);
+      sd = sd + nw;
+      rot[k * NS + j] = cu;
+    }
+  }
+}
+
 // Four-wave form of k_pfd_dmprof for profiles of <= 128 bins (the same arithmetic, bit for
 // bit).  The single-wave kernel streamed the fold with one dependent load per lane at a time
 // and swept the 100 trial DMs one after another; here
-//   * all 256 threads reduce the fold over its parts, 4 elements x 4 parts of independent
-//     loads in flight per thread (each element still sums its parts in order, as numpy);
-//   * wave 1 tabulates the accumulated sub-band rotations of all 100 trial DMs;
+//   * all 256 threads reduce the fold over its parts, 8 elements x 2 parts of loads in
+//     flight per thread (each element still sums its parts in order, as numpy);
+//   * wave 3 tabulates the accumulated sub-band rotations of all 100 trial DMs while its
+//     first loads are in flight;
 //   * the sweep runs 32 trial DMs at a time, 8 lanes per DM: lane a accumulates numpy's
 //     pairwise-leaf partial r_a = x_a + x_{a+8} + ... of the DM's chi^2 terms directly from
 //     the sub-band rows in LDS, and the 8 partials combine in numpy's order;
 //   * wave 0 builds the profile and finishes the fold (statistics, 22-score parameters) as
 //     the single-wave kernel.
-__global__ __launch_bounds__(256) void k_pfd_dmprof4(PfdArgs a) {
+__global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   extern __shared__ double lds[];
   const int64_t c = blockIdx.x;
   if (c >= a.n) return;
@@ -533,16 +556,19 @@ __global__ __launch_bounds__(256) void k_pfd_dmprof4(PfdArgs a) {
     }
   }
   __syncthreads();
-  // T[j][b] = sum over parts of the rotated sub-integration profiles (profs.sum(0))
+  // T[j][b] = sum over parts of the rotated sub-integration profiles (profs.sum(0)): each
+  // thread keeps PFD4_E elements and walks the parts, so PFD4_E loads are in flight per
+  // thread and step; wave 3 first tabulates the sweep's rotations (below), overlapping them
+  // with its first loads
   {
     const int total = NS * L;
     const int64_t pstride = (int64_t)NS * L;
-    for (int e0 = tid; e0 < total; e0 += 256 * 4) {
-      int src[4];
-      bool ok[4];
-      double acc[4];
+    for (int e0 = tid; e0 < total; e0 += 256 * PFD4_E) {
+      int src[PFD4_E];
+      bool ok[PFD4_E];
+      double acc[PFD4_E];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < PFD4_E; ++u) {
         const int e = e0 + 256 * u;
         ok[u] = e < total;
         const int j = ok[u] ? e / L : 0;
@@ -551,36 +577,20 @@ __global__ __launch_bounds__(256) void k_pfd_dmprof4(PfdArgs a) {
         src[u] = j * L + (b + r < L ? b + r : b + r - L);
         acc[u] = ok[u] ? P[src[u]] : 0.0;
       }
-#pragma unroll 4
+      if (wv == 3 && sweep && e0 == tid) sweep_rotations(rot, sdb, fr, NS, L, bps, dm_lo, dm_hi, lane);
+#pragma unroll 2
       for (int p = 1; p < NP; ++p) {
-        double v[4];
+        double v[PFD4_E];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ok[u] ? P[p * pstride + src[u]] : 0.0;
+        for (int u = 0; u < PFD4_E; ++u) v[u] = ok[u] ? P[p * pstride + src[u]] : 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] += v[u];
+        for (int u = 0; u < PFD4_E; ++u) acc[u] += v[u];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < PFD4_E; ++u)
         if (ok[u]) T[e0 + 256 * u] = acc[u];
     }
-  }
-  __syncthreads();
-  if (wv == 1 && sweep) {
-    // the sweep's accumulated rotations (PFDFile.py:395-416): each lane follows its sub-bands
-    // through the 100 trial DMs
-    for (int j = lane; j < NS; j += 64) {
-      int cu = 0;
-      double sd = sdb[j];
-      for (int k = 0; k < PFE_PFD_NDM; ++k) {
-        const double dm = dm_lo + ((dm_hi - dm_lo) * (double)k) / (double)(PFE_PFD_NDM - 1);
-        const double hif = delay_from_dm(dm, fr[NS - 1]);
-        const double delaybins = (delay_from_dm(dm, fr[j]) - hif) * bps - sd;
-        const double nw = floor(delaybins + 0.5);
-        cu = pymod((long long)cu + (long long)nw, L);
-        sd = sd + nw;
-        rot[k * NS + j] = cu;
-      }
-    }
+    if (wv == 3 && sweep && tid >= total) sweep_rotations(rot, sdb, fr, NS, L, bps, dm_lo, dm_hi, lane);
   }
   __syncthreads();
   // ---- chi^2 versus DM over span(dms[0], dms[-1], 100) (PFDFile.py:378-423)
@@ -606,8 +616,30 @@ __global__ __launch_bounds__(256) void k_pfd_dmprof4(PfdArgs a) {
         if (ai == 0)
           for (int i = 0; i < L; ++i) res += xval(i);
       } else {
-        double r = xval(ai);
-        for (int b = 8 + ai; b < nb; b += 8) r += xval(b);
+        // the chi^2 terms x(8m + ai), m < nb/8, summed over the sub-bands in order with the
+        // 16 (or fewer) row reads of one sub-band independent of each other
+        const int nm = nb / 8;
+        double sm[16];
+        for (int j = 0; j < NS; ++j) {
+          const int r = rk[j];
+          const double* row = T + (size_t)j * L;
+#pragma unroll
+          for (int m = 0; m < 16; ++m)
+            if (m < nm) {
+              int src = 8 * m + ai + r;
+              if (src >= L) src -= L;
+              const double v = row[src];
+              sm[m] = (j == 0) ? v : sm[m] + v;
+            }
+        }
+        double r = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if (m < nm) {
+            const double d = sm[m] - avgprof;
+            const double x = (d * d) / varprof;
+            r = (m == 0) ? x : r + x;
+          }
         const int base = lane & ~7;
         const double r0 = __shfl(r, base + 0), r1 = __shfl(r, base + 1);
         const double r2 = __shfl(r, base + 2), r3 = __shfl(r, base + 3);
