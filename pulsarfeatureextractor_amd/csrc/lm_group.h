@@ -418,8 +418,17 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
   const int lane = lane_id();
   if (lane < FPW) ph[lane] = PH_DONE;  // every slot takes its first fit in the refill step
   blm_sync();
+#ifdef PFE_LM_PROFILE
+  // per-wave phase cycles, added to the global counters once at the end (slots 9 T-phase,
+  // 10 total, 11 refill, 12 SIMT, 13 O-phase; 14/15 fits per O / T round x 1000)
+  long long c_ref = 0, c_o = 0, c_s = 0, c_t = 0, n_o = 0, n_t = 0, r_o = 0, r_t = 0;
+  const long long c_start = lm_clock();
+#endif
   for (;;) {
     // refill slots whose fit has ended
+#ifdef PFE_LM_PROFILE
+    long long t0 = lm_clock();
+#endif
     const uint64_t done = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_DONE);
     for (uint64_t m = done; m; m &= m - 1) {
       const int f = __builtin_ctzll(m);
@@ -430,6 +439,11 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     blm_sync();
     const int myph = lane < FPW ? ph[lane] : PH_EMPTY;
     if (__ballot(myph != PH_EMPTY) == 0) break;
+#ifdef PFE_LM_PROFILE
+    long long t1 = lm_clock();
+    c_ref += t1 - t0;
+    t0 = t1;
+#endif
     // O-phase: fresh fits and accepted steps
     const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
     if (mo) {
@@ -440,12 +454,24 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
       blm_sync();
     }
+#ifdef PFE_LM_PROFILE
+    t1 = lm_clock();
+    c_o += t1 - t0;
+    t0 = t1;
+    n_o += __builtin_popcountll(mo);
+    r_o += (__builtin_popcountll(mo) + 3) / 4;
+#endif
     // SIMT phase: the gtol test after a new Jacobian, lmpar, the trial point
     if (lane < FPW && ph[lane] == PH_LMPAR) {
       blm_simt<N, FPW>(lane, S);
       ph[lane] = S.info[lane] != 0 ? PH_DONE : PH_TRIAL;
     }
     blm_sync();
+#ifdef PFE_LM_PROFILE
+    t1 = lm_clock();
+    c_s += t1 - t0;
+    t0 = t1;
+#endif
     // T-phase
     const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
     if (mt) {
@@ -455,7 +481,22 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
         if (glane() == 0) ph[f] = nph;
       });
     }
+#ifdef PFE_LM_PROFILE
+    c_t += lm_clock() - t0;
+    n_t += __builtin_popcountll(mt);
+    r_t += (__builtin_popcountll(mt) + 3) / 4;
+#endif
   }
+#ifdef PFE_LM_PROFILE
+  LM_ADD(9, c_t);
+  LM_ADD(10, lm_clock() - c_start);
+  LM_ADD(11, c_ref);
+  LM_ADD(12, c_s);
+  LM_ADD(13, c_o);
+  LM_ADD(14, r_o ? 1000 * n_o / r_o : 0);
+  LM_ADD(15, r_t ? 1000 * n_t / r_t : 0);
+  LM_ADD(0, 1);  // waves
+#endif
 }
 
 }  // namespace pfe

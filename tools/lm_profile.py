@@ -75,6 +75,17 @@ def main():
             per["cycles_per_iter"] = {nm[4:]: d[nm] / max(d["iters"], 1) for nm in NAMES[5:9]}
             per["cycles_per_iter"]["trial"] = d["cyc_trial"] / max(d["lmpar"], 1)
             per["cycles_per_qrsolv_call_lmpar"] = d["cyc_lmpar"] / max(d["lmpar"], 1)
+            if row[13] > 0:  # pooled group engine (lm_group.h): per-wave phase cycles
+                tot = row[10]
+                res[f"{tag}/N={npar}/pooled"] = {
+                    "waves": int(row[0]),
+                    "frac_refill": row[11] / tot, "frac_O_phase": row[13] / tot,
+                    "frac_SIMT": row[12] / tot, "frac_T_phase": row[9] / tot,
+                    "mean_fits_per_O_round": row[14] / 1000.0 / max(row[0], 1),
+                    "mean_fits_per_T_round": row[15] / 1000.0 / max(row[0], 1),
+                    "mcycles_per_wave": tot / max(row[0], 1) / 1e6,
+                }
+                continue
             if row[14] > 0:  # batched solver (lm_batch.h): per-wave phase cycles
                 per["batched"] = {
                     "simt_phases": int(row[14]),
