@@ -47,7 +47,9 @@ def parse():
                     help="candidates per GPU (default 10M for lyon8, 1M for bates22)")
     ap.add_argument("--lp", type=int, default=128)
     ap.add_argument("--ld", type=int, default=128)
-    ap.add_argument("--path", choices=["lyon8", "bates22", "pfd", "pfd22"], default="lyon8")
+    ap.add_argument("--path", choices=["lyon8", "bates22", "all30", "pfd", "pfd22"], default="lyon8",
+                    help="all30: config 5's 8 Lyon features + 22 Bates scores per candidate "
+                         "into one (n, 30) feature matrix")
     ap.add_argument("--pfd-shape", default="16x32x128", help="npart x nsub x proflen (pfd path)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
@@ -201,9 +203,11 @@ def load_ops_per_candidate():
 def main():
     args = parse()
     if args.n is None:
-        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "pfd": 32768, "pfd22": 32768}[args.path]
+        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "all30": 1_000_000, "pfd": 32768,
+                  "pfd22": 32768}[args.path]
     if args.cpu_sample is None:
-        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "pfd": 200, "pfd22": 60}[args.path]
+        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "all30": 300, "pfd": 200,
+                           "pfd22": 60}[args.path]
     pfd_shape = tuple(int(v) for v in args.pfd_shape.split("x"))
     import torch
     import torch.distributed as dist
@@ -276,8 +280,24 @@ def main():
         out = torch.empty((n, 22), dtype=torch.float64, device=dev)
         status = torch.empty((n,), dtype=torch.int32, device=dev)
 
-        def step():
-            eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out, status=status)
+        if args.path == "bates22":
+            def step():
+                eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out, status=status)
+        else:
+            # config 5: the profile of each candidate also feeds the Lyon features, with a
+            # 128-bin DM array per candidate; one (n, 30) feature matrix per step
+            _, dmrows = lyon_batch_torch(n, args.lp, args.ld, seed=20261020 + rank, device=dev)
+            o8 = torch.empty((n, 8), dtype=torch.float64, device=dev)
+            out = torch.empty((n, 30), dtype=torch.float64, device=dev)
+
+            def step():
+                eng.lyon8(bt["prof"], dmrows, out=o8)
+                eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out22,
+                            status=status)
+                out[:, :8].copy_(o8)
+                out[:, 8:].copy_(out22)
+
+            out22 = torch.empty((n, 22), dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -411,14 +431,20 @@ def main():
     else:
         ops = load_ops_per_candidate()
         achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
+        all30 = args.path == "all30"
         result = {
-            "metric": "candidates/sec (22-score path, 128-bin)",
+            "metric": ("candidates/sec (8+22-feature path, 128-bin)" if all30
+                       else "candidates/sec (22-score path, 128-bin)"),
             **common,
             "dtype": "f64",
             "config": {
-                "workload": f"config 3 shape: {n} synthetic candidates per GPU, {args.lp}-bin "
-                            f"profile, 16x{args.lp} sub-bands, 128-point DM curve, 22 Bates "
-                            f"scores (pfe_bates22)",
+                "workload": (f"config 5 shard: {n} synthetic candidates per GPU, {args.lp}-bin "
+                             f"profile + {args.ld}-bin DM array, 16x{args.lp} sub-bands, 128-point "
+                             f"DM curve, 8 Lyon + 22 Bates features into one (n, 30) matrix "
+                             f"(pfe_lyon8_u8 + pfe_bates22)") if all30 else
+                            (f"config 3 shape: {n} synthetic candidates per GPU, {args.lp}-bin "
+                             f"profile, 16x{args.lp} sub-bands, 128-point DM curve, 22 Bates "
+                             f"scores (pfe_bates22)"),
                 "candidates_per_gpu": n,
                 "profile_bins": args.lp,
                 "parallelism": f"candidate shards x{world}, no collective",
@@ -430,7 +456,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                 "traffic": None,
-                "kernel": "pfe_bates22 (8 kernels, one step)",
+                "kernel": ("pfe_lyon8_u8 + pfe_bates22, one step" if all30
+                           else "pfe_bates22 (8 kernels, one step)"),
                 "algorithmic_ops_per_candidate": ops,
                 "avg_step_ms": kern_ms,
                 "avg_step_ms_max_over_ranks": kern_ms_max,
@@ -458,6 +485,14 @@ def main():
             result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
         elif args.path == "pfd22":
             result["cpu_baseline"] = cpu_baseline_pfd22(pfd_shape, args.cpu_sample)
+        elif args.path == "all30":
+            b = cpu_baseline_bates22(args.lp, args.cpu_sample)
+            l8 = cpu_baseline_lyon8(args.lp, args.ld, 8000)
+            v = 1.0 / (1.0 / b["value"] + 1.0 / l8["value"])
+            result["cpu_baseline"] = {"value": v, "unit": "candidates/sec", "cores": 1,
+                                      "kind": "port",
+                                      "sample": f"{b['sample']}; plus {l8['sample']}; "
+                                                f"combined per-candidate time"}
         else:
             result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
     if rank == 0:
