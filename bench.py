@@ -98,6 +98,34 @@ def cpu_baseline_lyon8(lp, ld, sample):
     }
 
 
+def cpu_baseline_lyon8_omp(lp, ld, sample=2_000_000):
+    """the C restatement (oracle/c/lyon8_omp.c) with OpenMP on the host
+    cores this job has (OMP_NUM_THREADS, 16 on the GPU box); None when it is not built."""
+    from oracle import lyon_c
+    from pulsarfeatureextractor_amd.synth import lyon_batch
+
+    if not lyon_c.available():
+        return None
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    prof, dm = lyon_batch(sample, lp, ld, seed=4244)
+    lyon_c.lyon8_omp(prof[:10000], dm[:10000], threads)  # warm the thread pool
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        lyon_c.lyon8_omp(prof, dm, threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {
+        "value": sample / best,
+        "unit": "candidates/sec",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample} synthetic {lp}-bin profile + {ld}-bin DM rows through the C "
+                  f"restatement (oracle/c/lyon8_omp.c, two-pass float64 moments), best of 3, "
+                  f"{best * 1e3:.0f} ms on {threads} OpenMP threads",
+    }
+
+
 def cpu_baseline_bates22(lp, sample):
     import warnings
 
@@ -481,6 +509,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         if args.path == "lyon8":
             result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
+            omp = cpu_baseline_lyon8_omp(args.lp, args.ld)
+            if omp is not None:
+                result["cpu_baseline_multicore"] = omp
         elif args.path == "pfd":
             result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
         elif args.path == "pfd22":

@@ -184,3 +184,16 @@ def test_wide_histograms_vs_oracle(engine):
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
     check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor)
+
+
+def test_pooled_tiny_and_empty_batches(engine):
+    """Pools with fewer candidates than slots (1, 3, 33 rows) give every candidate the scores
+    it gets in a large batch; an empty batch is a no-op."""
+    b = bates_batch(200, seed=41)
+    full, sf = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    for k in (1, 3, 33):
+        o, s = engine.bates22(b["prof"][:k], b["sub"][:k], b["dmcurve"][:k], b["scal"][:k])
+        assert np.array_equal(s, sf[:k])
+        assert np.array_equal(np.nan_to_num(o, nan=7.0), np.nan_to_num(full[:k], nan=7.0)), k
+    o, s = engine.bates22(b["prof"][:0], b["sub"][:0], b["dmcurve"][:0], b["scal"][:0])
+    assert o.shape == (0, 22) and s.shape == (0,)
