@@ -245,11 +245,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    # PFE_BENCH_BACKEND=gloo (rehearsal only): N ranks sharing the GPUs there are, the
+    # barrier / max-over-ranks reduction over gloo; the driver's runs use RCCL ("nccl")
+    backend = os.environ.get("PFE_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist_on = world > 1
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from pulsarfeatureextractor_amd._native import Engine
     from pulsarfeatureextractor_amd.synth import lyon_batch_torch
@@ -351,7 +359,12 @@ def main():
 
     if dist_on:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if backend == "nccl":
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        else:
+            tc = t.cpu()
+            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+            t = tc
         elapsed, kern_ms_max = float(t[0]), float(t[1])
     else:
         kern_ms_max = kern_ms
