@@ -30,6 +30,24 @@ __device__ double np_leaf(const double* a, int n, int lane) {
   return res;
 }
 
+// np_leaf for 8 <= n <= 128 with every load of a lane issued before its adds (the same
+// order of additions, so the same bits)
+__device__ __forceinline__ double np_leaf128(const double* a, int n, int lane) {
+  const int nb = n - (n % 8);
+  double v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = a[min((lane & 7) + 8 * m, n - 1)];
+  double r = v[0];
+#pragma unroll
+  for (int m = 1; m < 16; ++m)
+    if (8 * m < nb) r += v[m];
+  const double r0 = bcast(r, 0), r1 = bcast(r, 1), r2 = bcast(r, 2), r3 = bcast(r, 3);
+  const double r4 = bcast(r, 4), r5 = bcast(r, 5), r6 = bcast(r, 6), r7 = bcast(r, 7);
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (int i = nb; i < n; ++i) res += a[i];
+  return res;
+}
+
 template <int D>
 __device__ __noinline__ double np_pairwise(const double* a, int n, int lane) {
   if (n <= 128) return np_leaf(a, n, lane);

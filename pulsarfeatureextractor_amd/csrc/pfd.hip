@@ -512,9 +512,9 @@ __device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, con
 //     flight per thread (each element still sums its parts in order, as numpy);
 //   * wave 3 tabulates the accumulated sub-band rotations of all 100 trial DMs while its
 //     first loads are in flight;
-//   * the sweep runs 32 trial DMs at a time, 8 lanes per DM: lane a accumulates numpy's
-//     pairwise-leaf partial r_a = x_a + x_{a+8} + ... of the DM's chi^2 terms directly from
-//     the sub-band rows in LDS, and the 8 partials combine in numpy's order;
+//   * the sweep runs 4 trial DMs at a time, one per wave: the lanes sum the rotated sub-band
+//     rows bin by bin (64 consecutive doubles of a row per read, so the LDS reads are
+//     conflict-free) and numpy's pairwise leaf sums the chi^2 terms;
 //   * wave 0 builds the profile and finishes the fold (statistics, 22-score parameters) as
 //     the single-wave kernel.
 __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
@@ -533,6 +533,7 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   double* bv = sdb + NS;             // NS
   int* cum = (int*)(bv + NS);        // NS
   int* rot = cum + NS;               // PFE_PFD_NDM x NS accumulated rotations of the sweep
+  double* xbuf = bv + NS + ((PFE_PFD_NDM + 1) * NS + 1) / 2;  // 4 x 128, after cum and rot
   __shared__ float chs[PFE_PFD_NDM], ftmp[PFE_PFD_NDM];
   const double* sc = a.scal + c * PFE_PFD_NSCAL;
   const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
@@ -593,67 +594,56 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
     if (wv == 3 && sweep && tid >= total) sweep_rotations(rot, sdb, fr, NS, L, bps, dm_lo, dm_hi, lane);
   }
   __syncthreads();
-  // ---- chi^2 versus DM over span(dms[0], dms[-1], 100) (PFDFile.py:378-423)
+  // ---- chi^2 versus DM over span(dms[0], dms[-1], 100) (PFDFile.py:378-423): each wave
+  // takes every 4th trial DM; its lanes sum the rotated sub-band rows over the bins (a wave
+  // reads 64 consecutive doubles of a row at a time), the chi^2 terms go to the wave's LDS
+  // row and numpy's pairwise leaf sums them (np_leaf, lanes 0-7)
   if (sweep) {
-    const int g = tid >> 3, ai = tid & 7;
-    const int nb = L - (L % 8);
-    for (int k = g; k < PFE_PFD_NDM; k += 256 / 8) {
+    double* xb = xbuf + wv * 128;
+    const int b0 = lane, b1 = lane + 64;
+    for (int k = wv; k < PFE_PFD_NDM; k += 4) {
       const int* rk = rot + k * NS;
-      auto xval = [&](int b) {
-        double s = 0.0;
-        for (int j = 0; j < NS; ++j) {
-          int src = b + rk[j];
-          if (src >= L) src -= L;
-          const double v = T[(size_t)j * L + src];
-          s = (j == 0) ? v : s + v;
-        }
-        const double d = s - avgprof;
-        return (d * d) / varprof;
-      };
-      double res;
-      if (L < 8) {  // np_leaf, n < 8
-        res = 0.0;
-        if (ai == 0)
-          for (int i = 0; i < L; ++i) res += xval(i);
-      } else {
-        // the chi^2 terms x(8m + ai), m < nb/8, summed over the sub-bands in order with the
-        // 16 (or fewer) row reads of one sub-band independent of each other
-        const int nm = nb / 8;
-        double sm[16];
-        for (int j = 0; j < NS; ++j) {
-          const int r = rk[j];
-          const double* row = T + (size_t)j * L;
+      // 8 sub-bands per step: their rotations, then all 16 row reads, then the ordered adds
+      // (unconditional reads at clamped indices keep every load of a step in flight)
+      double s0 = 0.0, s1 = 0.0;
+      const int b0c = b0 < L ? b0 : 0, b1c = b1 < L ? b1 : 0;
+      for (int j0 = 0; j0 < NS; j0 += 8) {
+        int r[8];
 #pragma unroll
-          for (int m = 0; m < 16; ++m)
-            if (m < nm) {
-              int src = 8 * m + ai + r;
-              if (src >= L) src -= L;
-              const double v = row[src];
-              sm[m] = (j == 0) ? v : sm[m] + v;
-            }
-        }
-        double r = 0.0;
+        for (int u = 0; u < 8; ++u) r[u] = rk[min(j0 + u, NS - 1)];
+        double v0[8], v1[8];
 #pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (m < nm) {
-            const double d = sm[m] - avgprof;
-            const double x = (d * d) / varprof;
-            r = (m == 0) ? x : r + x;
+        for (int u = 0; u < 8; ++u) {
+          const double* row = T + (size_t)min(j0 + u, NS - 1) * L;
+          int i0 = b0c + r[u];
+          if (i0 >= L) i0 -= L;
+          int i1 = b1c + r[u];
+          if (i1 >= L) i1 -= L;
+          v0[u] = row[i0];
+          v1[u] = row[i1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (j0 + u < NS) {
+            s0 = (j0 + u == 0) ? v0[u] : s0 + v0[u];
+            s1 = (j0 + u == 0) ? v1[u] : s1 + v1[u];
           }
-        const int base = lane & ~7;
-        const double r0 = __shfl(r, base + 0), r1 = __shfl(r, base + 1);
-        const double r2 = __shfl(r, base + 2), r3 = __shfl(r, base + 3);
-        const double r4 = __shfl(r, base + 4), r5 = __shfl(r, base + 5);
-        const double r6 = __shfl(r, base + 6), r7 = __shfl(r, base + 7);
-        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-        if (ai == 0)
-          for (int i = nb; i < L; ++i) res += xval(i);
       }
-      if (ai == 0) {
-        const float chi = (float)(res / ((double)L - 1.0));
-        chs[k] = chi;
-        if (a.chis) a.chis[c * PFE_PFD_NDM + k] = chi;
+      if (b0 < L) {
+        const double d = s0 - avgprof;
+        xb[b0] = (d * d) / varprof;
       }
+      if (b1 < L) {
+        const double d = s1 - avgprof;
+        xb[b1] = (d * d) / varprof;
+      }
+      lds_sync();
+      const double chi = (L >= 8 ? np_leaf128(xb, L, lane) : np_leaf(xb, L, lane)) / ((double)L - 1.0);
+      if (lane == 0) {
+        chs[k] = (float)chi;
+        if (a.chis) a.chis[c * PFE_PFD_NDM + k] = (float)chi;
+      }
+      lds_sync();
     }
   }
   __syncthreads();
@@ -695,7 +685,8 @@ size_t pfd_lds_bytes(int nsub, int L) {
 }
 
 static size_t pfd4_lds_bytes(int nsub, int L) {
-  return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int);
+  return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int) + 8 +
+         4 * 128 * sizeof(double);
 }
 
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {
