@@ -85,6 +85,7 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());
   a.gslots = glm_slots(n, device_cus());
+  a.cus = device_cus();
   a.lp = lp;
   a.n = n;
   // Python evaluates pow(len(data), -0.3333333) with the C library; so does this host code

@@ -54,6 +54,7 @@ struct BatesArgs {
   int fpw;             // fits per wave of the batched kernels (<= BLM_FPW): small batches
                        // use fewer so that there are several waves per wave slot
   int gslots;          // fit slots per wave of the pooled kernels (<= GLM_FPW)
+  int cus;             // compute units of the device
 };
 
 constexpr int BATES_NCOUNTERS = 16;
@@ -72,6 +73,14 @@ __host__ __device__ constexpr int profile_mpl(int lp) {
 // per-wave scratch of k_gdgb: x and y of FPW fits, 64*MPL rows each
 __host__ __device__ constexpr size_t gdg_wave_scratch_doubles(int lp) {
   return (size_t)BLM_FPW * 64 * profile_mpl(lp) * 2;
+}
+
+// persistent waves of a pooled kernel without per-wave scratch that holds `per_simd` waves
+// per SIMD: enough to fill the device, never more than the slots the batch needs
+static inline dim3 pool_grid(const BatesArgs& a, int per_simd) {
+  const int64_t need = (a.n + a.gslots - 1) / a.gslots;
+  const int64_t cap = (int64_t)a.cus * 4 * per_simd;
+  return dim3((unsigned)(need < cap ? (need > 0 ? need : 1) : cap));
 }
 
 static inline dim3 grid_for_candidates(int64_t n) {

@@ -372,7 +372,7 @@ struct SineProb {
 };
 
 template <int MPL, bool F>
-__global__ __launch_bounds__(64, 2) void k_sineg(BatesArgs a) {
+__global__ __launch_bounds__(64, 3) void k_sineg(BatesArgs a) {
   constexpr int FPW = GLM_FPW;
   __shared__ BlmState<2, FPW> S;
   __shared__ SlotTab<FPW> T;
@@ -613,7 +613,7 @@ struct DMProb {
 };
 
 template <int MPL>
-__global__ __launch_bounds__(64, 2) void k_dmfitg(BatesArgs a) {
+__global__ __launch_bounds__(64, 3) void k_dmfitg(BatesArgs a) {
   constexpr int FPW = GLM_FPW;
   __shared__ BlmState<3, FPW> S;
   __shared__ SlotTab<FPW> T;
@@ -1060,9 +1060,9 @@ template <bool F>
 static void launch_sine_t(const BatesArgs& a, hipStream_t st) {
   if (glm_on() && a.lp <= 128) {
     if (a.lp <= 64)
-      hipLaunchKernelGGL((k_sineg<1, F>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((k_sineg<1, F>), pool_grid(a, 3), dim3(64), 0, st, a);
     else
-      hipLaunchKernelGGL((k_sineg<2, F>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((k_sineg<2, F>), pool_grid(a, 3), dim3(64), 0, st, a);
     return;
   }
   if (a.lp <= 64)
@@ -1087,9 +1087,9 @@ hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
   const char* blm_env = getenv("PFE_BLM");
   if (glm_on() && a.ndm <= 128) {
     if (a.ndm <= 64)
-      hipLaunchKernelGGL(k_dmfitg<1>, dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+      hipLaunchKernelGGL(k_dmfitg<1>, pool_grid(a, 3), dim3(64), 0, st, a);
     else
-      hipLaunchKernelGGL(k_dmfitg<2>, dim3((unsigned)a.pwaves), dim3(64), 0, st, a);
+      hipLaunchKernelGGL(k_dmfitg<2>, pool_grid(a, 3), dim3(64), 0, st, a);
     return hipGetLastError();
   }
   if (!(blm_env && blm_env[0] == '0')) {  // batched lmdif (lm_batch.h)
