@@ -93,7 +93,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
         list(ex.map(run, jobs))
     if force or jobs or not os.path.exists(lib):
         tmp = lib + ".tmp"
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lz", "-pthread"])
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lz", "-ldl", "-pthread"])
         os.replace(tmp, lib)
     return lib
 

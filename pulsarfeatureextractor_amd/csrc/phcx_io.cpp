@@ -10,6 +10,7 @@
 // that (comments / CDATA / child elements inside a leaf, non-ASCII text, unusual number
 // spellings) is reported as a per-file status so the host can use its Python parser for
 // that file instead of guessing.
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -52,6 +53,69 @@ struct ThreadBuffers {
 };
 thread_local ThreadBuffers tls;
 
+// ---- libdeflate (when the system has it): whole-buffer gzip inflate, 2-3x zlib's speed ----
+// Bound at run time through dlopen so that the library stays optional; PFE_NO_LIBDEFLATE=1
+// keeps zlib (A/B runs and tests).  Any result other than success falls back to the zlib
+// path, so malformed files fail exactly as before.
+struct Deflate {
+  using alloc_t = void* (*)();
+  using free_t = void (*)(void*);
+  using gz_t = int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);
+  alloc_t alloc = nullptr;
+  free_t release = nullptr;
+  gz_t gzip_ex = nullptr;
+  Deflate() {
+    void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc = (alloc_t)dlsym(h, "libdeflate_alloc_decompressor");
+    release = (free_t)dlsym(h, "libdeflate_free_decompressor");
+    gzip_ex = (gz_t)dlsym(h, "libdeflate_gzip_decompress_ex");
+    if (!alloc || !release || !gzip_ex) alloc = nullptr;
+  }
+};
+const Deflate& deflate_lib() {
+  static const Deflate d;
+  return d;
+}
+struct ThreadDecompressor {
+  void* d = nullptr;
+  ~ThreadDecompressor() {
+    if (d) deflate_lib().release(d);
+  }
+};
+thread_local ThreadDecompressor tls_dec;
+
+// all gzip members of raw into out[0, used); false: let zlib decide
+bool inflate_libdeflate(const std::string& raw, std::string& out, size_t& used) {
+  const Deflate& L = deflate_lib();
+  if (!L.alloc) return false;
+  const char* e = std::getenv("PFE_NO_LIBDEFLATE");
+  if (e && e[0] == '1') return false;
+  if (!tls_dec.d) tls_dec.d = L.alloc();
+  if (!tls_dec.d) return false;
+  size_t pos = 0;
+  used = 0;
+  for (;;) {
+    size_t in_used = 0, out_used = 0;
+    int rc;
+    for (;;) {
+      if (out.size() - used < raw.size() * 4 + (1 << 16))
+        out.resize(std::max(out.size() * 2, used + raw.size() * 4 + (1 << 16)));
+      rc = L.gzip_ex(tls_dec.d, raw.data() + pos, raw.size() - pos, &out[used], out.size() - used,
+                     &in_used, &out_used);
+      if (rc != 3) break;  // LIBDEFLATE_INSUFFICIENT_SPACE: a larger buffer, the member again
+      out.resize(out.size() * 2);
+    }
+    if (rc != 0) return false;
+    pos += in_used;
+    used += out_used;
+    // another gzip member may follow; trailing zero padding is tolerated like Python's
+    size_t k = pos;
+    while (k < raw.size() && raw[k] == 0) ++k;
+    if (k == raw.size()) return true;
+  }
+}
+
 bool read_all(const char* path, bool gz, std::string& out, int& err) {
   FILE* f = std::fopen(path, "rb");
   if (!f) {
@@ -79,6 +143,13 @@ bool read_all(const char* path, bool gz, std::string& out, int& err) {
   if (raw.size() < 2 || (uint8_t)raw[0] != 0x1f || (uint8_t)raw[1] != 0x8b) {
     err = PFE_IO_ERR_GZIP;
     return false;
+  }
+  {
+    size_t used = 0;
+    if (inflate_libdeflate(raw, out, used)) {
+      out.resize(used);
+      return true;
+    }
   }
   z_stream zs;
   std::memset(&zs, 0, sizeof zs);

@@ -153,3 +153,25 @@ def test_pack_matches_fetch(tmp_path):
         assert np.array_equal(out["scal"][i], c.scal)
     with pytest.raises(_native.PfeError):
         b.pack(rows, lp=inf.lp - 1)
+
+
+def test_libdeflate_and_zlib_paths_agree(tmp_path, monkeypatch):
+    """The reader inflates with libdeflate when the system has it and falls back to zlib
+    (PFE_NO_LIBDEFLATE=1, or any libdeflate error): both give identical documents, also for
+    multi-member gzip files with trailing zero padding."""
+    paths = _write_golden(tmp_path, "bates22_phcx128", range(0, 40, 7))
+    # a two-member file with zero padding (Python's gzip module reads it)
+    raw = gzip.decompress(open(paths[0], "rb").read())
+    half = len(raw) // 2
+    multi = os.path.join(tmp_path, "multi.phcx.gz")
+    with open(multi, "wb") as f:
+        f.write(gzip.compress(raw[:half]) + gzip.compress(raw[half:]) + b"\0" * 16)
+    paths.append(multi)
+    monkeypatch.setenv("PFE_NO_LIBDEFLATE", "1")
+    z = processor.parse_all(paths, workers=2, native=True)
+    monkeypatch.setenv("PFE_NO_LIBDEFLATE", "0")
+    d = processor.parse_all(paths, workers=2, native=True)
+    for (a, ea), (c, ec) in zip(z, d):
+        assert ea is None and ec is None
+        _same(a, c)
+    _same(d[-1][0], d[0][0])
