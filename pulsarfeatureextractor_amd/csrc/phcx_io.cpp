@@ -273,6 +273,21 @@ void scan(const std::string& d, std::vector<Elem> (&occ)[NTAGS]) {
 // element text as ElementTree delivers it: CRLF / CR -> LF, entities decoded.
 // Returns false (fallback) for non-ASCII text or an unknown entity.
 bool element_text(const std::string& d, const Elem& e, std::string& out) {
+  // fast path: plain ASCII without CR or entities (every PHCX element in practice) is
+  // delivered as it stands
+  {
+    const unsigned char* p = (const unsigned char*)d.data() + e.tb;
+    const size_t len = e.te - e.tb;
+    unsigned special = 0;
+    for (size_t k = 0; k < len; ++k) {
+      const unsigned c = p[k];
+      special |= (c >= 0x80u) | (c == (unsigned)'\r') | (c == (unsigned)'&');
+    }
+    if (!special) {
+      out.assign((const char*)p, len);
+      return true;
+    }
+  }
   out.clear();
   out.reserve(e.te - e.tb);
   for (size_t i = e.tb; i < e.te; ++i) {
@@ -339,33 +354,45 @@ bool py_int_hex(const char* s, size_t len, int& v) {
 
 // hex decode with the reference's loop (PHCXFile.py:144-186, PHCXOperations.py:263-297):
 // skip '\n', take text[i:i+2], stop at the first slice int() rejects
+struct HexLut {
+  int8_t v[256];
+  HexLut() {
+    for (int c = 0; c < 256; ++c) v[c] = (int8_t)hexval((char)c);
+  }
+};
+const HexLut kHex;
+
 bool hex_decode(const std::string& t, std::vector<uint8_t>& out, int& err) {
-  out.clear();
-  out.reserve(t.size() / 2);
   const size_t n = t.size();
+  out.resize(n / 2 + 1);
+  uint8_t* o = out.data();
+  size_t m = 0;
+  const unsigned char* s = (const unsigned char*)t.data();
   size_t i = 0;
   while (i < n) {
-    if (t[i] == '\n') {
+    if (s[i] == '\n') {
       ++i;
       continue;
     }
-    int v;
     if (i + 1 < n) {
-      const int h0 = hexval(t[i]), h1 = hexval(t[i + 1]);
-      if (h0 >= 0 && h1 >= 0) {
-        out.push_back((uint8_t)(h0 * 16 + h1));
+      const int h0 = kHex.v[s[i]], h1 = kHex.v[s[i + 1]];
+      if ((h0 | h1) >= 0) {
+        o[m++] = (uint8_t)(h0 * 16 + h1);
         i += 2;
         continue;
       }
     }
+    int v;
     if (!py_int_hex(t.data() + i, std::min<size_t>(2, n - i), v)) break;
     if (v < 0 || v > 255) {
       err = PFE_IO_ERR_RANGE;
+      out.resize(m);
       return false;
     }
-    out.push_back((uint8_t)v);
+    o[m++] = (uint8_t)v;
     i += 2;
   }
+  out.resize(m);
   return true;
 }
 
