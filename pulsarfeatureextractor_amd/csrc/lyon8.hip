@@ -507,10 +507,16 @@ __global__ __launch_bounds__(256) void lyon8_f64_generic(const double* __restric
 namespace pfe {
 
 static inline int grid_for(int64_t work_waves) {
-  // 4 waves per block; cap at 256 CUs x 8 blocks and grid-stride the rest.
+  // 4 waves per block; cap at 256 CUs x 32 blocks (7 resident waves per SIMD at 71 VGPRs: +1-2 % over
+  // 8 blocks per CU, tools/ab_lyon8_grid.sh) and grid-stride the rest
+  // (PFE_LYON8_BLOCKS overrides the cap: A/B runs)
+  static const int64_t cap = [] {
+    const char* v = getenv("PFE_LYON8_BLOCKS");
+    return (int64_t)(v && atoi(v) > 0 ? atoi(v) : 8192);
+  }();
   int64_t blocks = (work_waves + 3) / 4;
   if (blocks < 1) blocks = 1;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > cap) blocks = cap;
   return (int)blocks;
 }
 
