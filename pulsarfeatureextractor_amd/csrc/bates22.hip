@@ -93,8 +93,25 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
   a.c_lp1 = std::pow((double)(lp - 1), -0.3333333);
 }
 
+// fork the three independent score groups onto the handle's side streams (false: serial,
+// when the handle has none or PFE_SERIAL=1)
+bool fork_begin(const Fork* fk, hipStream_t st) {
+  const char* e = getenv("PFE_SERIAL");
+  if (!fk || !fk->side[0] || (e && e[0] == '1')) return false;
+  if (hipEventRecord(fk->ev[0], st) != hipSuccess) return false;
+  return hipStreamWaitEvent(fk->side[0], fk->ev[0], 0) == hipSuccess &&
+         hipStreamWaitEvent(fk->side[1], fk->ev[0], 0) == hipSuccess;
+}
+hipError_t fork_end(const Fork* fk, hipStream_t st) {
+  hipError_t e;
+  if ((e = hipEventRecord(fk->ev[1], fk->side[0])) != hipSuccess) return e;
+  if ((e = hipEventRecord(fk->ev[2], fk->side[1])) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(st, fk->ev[1], 0)) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, fk->ev[2], 0);
+}
+
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
-                          size_t work_bytes, hipStream_t st) {
+                          size_t work_bytes, hipStream_t st, const Fork* fk) {
   if (work_bytes < bates22_workspace_bytes(in)) return hipErrorInvalidValue;
   BatesArgs a;
   bates_setup(a, in->n, in->lp, work);
@@ -116,10 +133,18 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.counters, 0, BATES_NCOUNTERS * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
-  if ((e = launch_sine(a, st)) != hipSuccess) return e;
-  if ((e = launch_gauss(a, st)) != hipSuccess) return e;
-  if ((e = launch_dmfit(a, st)) != hipSuccess) return e;
-  if ((e = launch_subband(a, st)) != hipSuccess) return e;
+  if (fork_begin(fk, st)) {
+    if ((e = launch_gauss(a, fk->side[0])) != hipSuccess) return e;
+    if ((e = launch_dmfit(a, fk->side[1])) != hipSuccess) return e;
+    if ((e = launch_subband(a, fk->side[1])) != hipSuccess) return e;
+    if ((e = launch_sine(a, st)) != hipSuccess) return e;
+    if ((e = fork_end(fk, st)) != hipSuccess) return e;
+  } else {
+    if ((e = launch_sine(a, st)) != hipSuccess) return e;
+    if ((e = launch_gauss(a, st)) != hipSuccess) return e;
+    if ((e = launch_dmfit(a, st)) != hipSuccess) return e;
+    if ((e = launch_subband(a, st)) != hipSuccess) return e;
+  }
   launch_clear_internal(status, in->n, st);
   return hipGetLastError();
 }

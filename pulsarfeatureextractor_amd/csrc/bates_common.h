@@ -58,6 +58,14 @@ struct BatesArgs {
 };
 
 constexpr int BATES_NCOUNTERS = 16;
+
+// Side streams of a handle: the score groups that do not depend on each other run on them
+// concurrently with the caller's stream (sine fits | Gaussian chain | DM fit + sub-bands), so
+// one kernel's drain tail overlaps another's work.  Status bits are set with atomics.
+struct Fork {
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
 constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
 constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS state size)
 constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernels (lm_group.h)

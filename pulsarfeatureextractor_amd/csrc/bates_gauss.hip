@@ -472,18 +472,18 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   const int lp = a.lp;
   GhPre<P, F> g;
   ghist_prologue<P, F>(a, c, g);
-  if (D64 && lane == 0) a.status[c] &= ~ST_DEFER_HIST64;
+  if (D64 && lane == 0) atomicAnd(&a.status[c], ~(uint32_t)(ST_DEFER_HIST64));
   if (g.nan) {  // numpy.histogram: autodetected range is not finite (ValueError)
-    if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_GAUSS_FAIL));
     return;
   }
   const int hb = g.hb, db = g.db;
   uint32_t st = 0;
   if (hb <= 0 || db <= 0) st = PFE_ST_GAUSS_FAIL;                  // histogram(bins=0) raises
   if (!st && (hb > 64 * H || db > 64 * H)) st = BIG ? PFE_ST_UNSUPPORTED : ST_DEFER_HIST;
-  if (BIG && lane == 0) a.status[c] &= ~ST_DEFER_HIST;
+  if (BIG && lane == 0) atomicAnd(&a.status[c], ~(uint32_t)(ST_DEFER_HIST));
   if (st) {
-    if (lane == 0) a.status[c] |= st;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(st));
     return;
   }
   // ---- derivative histogram and its fit (:657-661)
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   }
   const HistFit fp = fit_gaussian_hist<H>(fn, hb, lane);
   if (fd.fail || fp.fail || hb < 2) {  // hb < 2: leastsq(m=1 < n=2) raises TypeError
-    if (lane == 0) a.status[c] |= PFE_ST_GAUSS_FAIL;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_GAUSS_FAIL));
     return;
   }
   // fixed-mean fit (:1034-1045): xmax = xData[int(bins/2)-1] (index -1 = last bin)
@@ -650,7 +650,7 @@ struct GhistProb {
         return true;
       }
       if (fail) {
-        if (lane == 0) a.status[c0] |= PFE_ST_GAUSS_FAIL;
+        if (lane == 0) atomicOr(&a.status[c0], (uint32_t)(PFE_ST_GAUSS_FAIL));
       } else if (st == 0) {
         if (lane == 0) a.ws[c0].fd_mu = p[1];
         start(1, f, S, 0, 0.0);
@@ -679,7 +679,7 @@ struct GhistProb {
         if (g.nan || g.hb <= 0 || g.db <= 0 || g.hb < 2) stt = PFE_ST_GAUSS_FAIL;
         else if (g.hb > 64 || g.db > 64) stt = ST_DEFER_HIST64;
         if (stt) {
-          if (lane == 0) a.status[c] |= stt;
+          if (lane == 0) atomicOr(&a.status[c], (uint32_t)(stt));
           continue;
         }
         const HistSpec hd = hist_spec(g.dmin, g.dmax, g.db);
@@ -1246,7 +1246,7 @@ __device__ __forceinline__ int gdg_peel(const BatesArgs& a, int64_t c, double* y
     if (lane == 0) {
       a.out[c * 22 + 9] = 1000000.0;
       a.out[c * 22 + 10] = 1000000.0;
-      a.status[c] |= PFE_ST_DGF_INDEXERROR;
+      atomicOr(&a.status[c], (uint32_t)(PFE_ST_DGF_INDEXERROR));
     }
     return -1;
   }

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
   double yv[MPL];
   const SinePre pre = sine_prologue<MPL, F>(a, c, stage_all[threadIdx.x >> 6], yv);
   if (pre.fail) {
-    if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SINE_FAIL));
     return;
   }
   const double c1 = sine_chisq<MPL, false>(yv, lp, lane, pre.h, pre.maxima, pre.y0);
@@ -327,7 +327,7 @@ struct SineProb {
         double yv[MPL];
         const SinePre pre = sine_prologue<MPL, F>(a, c, sg, yv);
         if (pre.fail) {
-          if (lane == 0) a.status[c] |= PFE_ST_SINE_FAIL;
+          if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SINE_FAIL));
           continue;
         }
         double q[2];
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
   if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;                       // corrcoef length mismatch
   if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
   if (fail) {
-    if (lane == 0) a.status[c] |= fail;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(fail));
     return;
   }
   const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
     }
   }
   if (m == 0) {  // ZeroDivisionError (:1681)
-    if (lane == 0) a.status[c] |= PFE_ST_SUBBAND_FAIL;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SUBBAND_FAIL));
     return;
   }
   const double mean_corr = csum / (double)m;
@@ -859,7 +859,7 @@ __global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
   if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;
   if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
   if (fail) {
-    if (lane == 0) a.status[c] |= fail;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(fail));
     return;
   }
   const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
     }
   }
   if (m == 0) {
-    if (lane == 0) a.status[c] |= PFE_ST_SUBBAND_FAIL;
+    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SUBBAND_FAIL));
     return;
   }
   const double mean_corr = csum / (double)m;

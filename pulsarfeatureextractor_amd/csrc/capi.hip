@@ -13,6 +13,7 @@
 #include <string>
 
 #include "../../include/pfe.h"
+#include "bates_common.h"
 #include "pfd.h"
 
 namespace pfe {
@@ -21,7 +22,7 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
 hipError_t launch_lyon8_f64(const double* prof, int64_t ps, int lp, const double* dm,
                             int64_t ds, int ld, int64_t n, double* out, hipStream_t st);
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
-                          size_t work_bytes, hipStream_t st);
+                          size_t work_bytes, hipStream_t st, const Fork* fk);
 size_t bates22_workspace_bytes(const pfe_bates_in* in);
 }  // namespace pfe
 
@@ -29,6 +30,7 @@ struct pfe_handle {
   int device = -1;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  pfe::Fork fork;  // side streams of the 22-score chains (bates_common.h)
   // staging scratch (device)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -107,6 +109,14 @@ int pfe_create(int device, pfe_handle** out) {
     return set_err(nullptr, PFE_EDEVICE, "pfe_create: %s", hipGetErrorString(e));
   }
   h->stream = h->own;
+  for (int i = 0; i < 2 && e == hipSuccess; ++i)
+    e = hipStreamCreateWithFlags(&h->fork.side[i], hipStreamNonBlocking);
+  for (int i = 0; i < 3 && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&h->fork.ev[i], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    pfe_destroy(h);
+    return set_err(nullptr, PFE_EDEVICE, "pfe_create: %s", hipGetErrorString(e));
+  }
   *out = h;
   return PFE_OK;
 }
@@ -116,6 +126,10 @@ void pfe_destroy(pfe_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->scratch) (void)hipFree(h->scratch);
+  for (hipStream_t& s : h->fork.side)
+    if (s) (void)hipStreamDestroy(s);
+  for (hipEvent_t& v : h->fork.ev)
+    if (v) (void)hipEventDestroy(v);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
@@ -270,7 +284,7 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
     int rc = ensure_scratch(h, work);
     if (rc) return rc;
   }
-  hipError_t e = pfe::launch_bates22(&din, dout, dstat, (char*)h->scratch + off, work, st);
+  hipError_t e = pfe::launch_bates22(&din, dout, dstat, (char*)h->scratch + off, work, st, &h->fork);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "bates22 launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -420,7 +434,7 @@ int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* 
     dstat = (uint32_t*)(base + off);
     off += tb;
   }
-  hipError_t e = pfe::launch_pfd22(a, dout, dstat, (char*)h->scratch + off, work, st);
+  hipError_t e = pfe::launch_pfd22(a, dout, dstat, (char*)h->scratch + off, work, st, &h->fork);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "pfd_bates22 launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));

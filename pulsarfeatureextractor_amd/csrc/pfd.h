@@ -27,7 +27,8 @@ size_t pfd_lds_bytes(int nsub, int L);
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st);
 // the 22-score chain (pfd22.hip); work: pfd22_workspace_bytes(n, L) bytes of device memory
 size_t pfd22_workspace_bytes(int64_t n, int L);
+struct Fork;
 hipError_t launch_pfd22(PfdArgs a, double* out, uint32_t* status, void* work, size_t work_bytes,
-                        hipStream_t st);
+                        hipStream_t st, const Fork* fk);
 
 }  // namespace pfe

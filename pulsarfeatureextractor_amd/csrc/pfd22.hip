@@ -24,6 +24,8 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
 size_t bates22_workspace_bytes(const pfe_bates_in* in);
 void bates_setup(BatesArgs& a, int64_t n, int lp, void* work);
 void launch_clear_internal(uint32_t* status, int64_t n, hipStream_t st);
+bool fork_begin(const Fork* fk, hipStream_t st);
+hipError_t fork_end(const Fork* fk, hipStream_t st);
 
 constexpr double KDM_PFD = 8.3 * 1000000.0;  // 8.3*10**6      (PFDOperations.py:342)
 constexpr double DF_PFD = 32.0;              // df = 32         (:343)
@@ -135,9 +137,10 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
   bool live = false;
   if (lane < a.fpw && base + lane < a.n) {
     uint32_t* st = a.status + base + lane;
-    if (*st & PFE_ST_PFD_DMCURVE_FAIL)  // numdms == 1: dms[0] raises in getDMFittings
-      *st = (*st & ~PFE_ST_PFD_DMCURVE_FAIL) | PFE_ST_DMFIT_FAIL;
-    else
+    if (*st & PFE_ST_PFD_DMCURVE_FAIL) {  // numdms == 1: dms[0] raises in getDMFittings
+      atomicAnd(st, ~(uint32_t)PFE_ST_PFD_DMCURVE_FAIL);  // (other score groups may be
+      atomicOr(st, (uint32_t)PFE_ST_DMFIT_FAIL);           // updating status concurrently)
+    } else
       live = true;
   }
   uint64_t fits = __ballot(live);
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
     pfd_dm_functor<MPL>(d, base + f, fn, pfd_dm_scale(d, base + f));
     double theo[MPL], amp0 = 0.0;
     if (!pfd_dm_theo<MPL>(fn, theo, amp0)) {  // ZeroDivisionError
-      if (lane == 0) a.status[base + f] |= PFE_ST_DMFIT_FAIL;
+      if (lane == 0) atomicOr(&a.status[base + f], (uint32_t)(PFE_ST_DMFIT_FAIL));
       fits &= ~(1ull << f);
       continue;
     }
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmfitb(PfdDMArgs d) {
       o[16] = fabs(1.0 - S.x[1][f]);                                   // s17 (:391)
       o[17] = fabs(S.x[2][f]);                                         // s18, filterScore(18)
       o[18] = ndeg ? chi / (double)ndeg : 0.0;                         // s19 (:387)
-      if (!ndeg) a.status[c] |= PFE_ST_DMFIT_FAIL;                     // ZeroDivisionError
+      if (!ndeg) atomicOr(&a.status[c], (uint32_t)(PFE_ST_DMFIT_FAIL));                     // ZeroDivisionError
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -241,7 +244,7 @@ __device__ __forceinline__ void pfd_dm_finish(const PfdDMArgs& d, int64_t c, dou
     o[16] = fabs(1.0 - prop);                                        // s17 (:391)
     o[17] = fabs(shift);                                             // s18, filterScore(18)
     o[18] = ndeg ? chi / (double)ndeg : 0.0;                         // s19 (:387)
-    if (!ndeg) a.status[c] |= PFE_ST_DMFIT_FAIL;                     // ZeroDivisionError
+    if (!ndeg) atomicOr(&a.status[c], (uint32_t)(PFE_ST_DMFIT_FAIL));                     // ZeroDivisionError
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -267,7 +270,10 @@ struct PfdDMProb {
         if (c >= a.n) break;
         const uint32_t st = a.status[c];
         if (st & PFE_ST_PFD_DMCURVE_FAIL) {  // numdms == 1: dms[0] raises in getDMFittings
-          if (lane == 0) a.status[c] = (st & ~PFE_ST_PFD_DMCURVE_FAIL) | PFE_ST_DMFIT_FAIL;
+          if (lane == 0) {
+            atomicAnd(&a.status[c], ~(uint32_t)PFE_ST_PFD_DMCURVE_FAIL);
+            atomicOr(&a.status[c], (uint32_t)PFE_ST_DMFIT_FAIL);
+          }
           continue;
         }
         const float sc = pfd_dm_scale(d, c);
@@ -275,7 +281,7 @@ struct PfdDMProb {
         pfd_dm_functor<MPL>(d, c, fn, sc);
         double theo[MPL], amp0 = 0.0;
         if (!pfd_dm_theo<MPL>(fn, theo, amp0)) {  // ZeroDivisionError
-          if (lane == 0) a.status[c] |= PFE_ST_DMFIT_FAIL;
+          if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_DMFIT_FAIL));
           continue;
         }
         if (lane == 0) {
@@ -333,7 +339,7 @@ static char* carve(char*& p, size_t bytes) {
 
 // pa: the PFD inputs (profs, subfreqs, scal, shape, n); out n x 22, status n (device)
 hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, size_t work_bytes,
-                        hipStream_t st) {
+                        hipStream_t st, const Fork* fk) {
   const int64_t n = pa.n;
   const int L = pa.L;
   if (work_bytes < pfd22_workspace_bytes(n, L)) return hipErrorInvalidValue;
@@ -365,16 +371,19 @@ hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, s
   a.status = status;
   e = hipMemsetAsync(a.counters, 0, BATES_NCOUNTERS * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
-  if ((e = launch_sine(a, st)) != hipSuccess) return e;
-  if ((e = launch_gauss(a, st)) != hipSuccess) return e;
+  const bool forked = fork_begin(fk, st);
+  const hipStream_t sg = forked ? fk->side[0] : st, sd = forked ? fk->side[1] : st;
+  if ((e = launch_gauss(a, sg)) != hipSuccess) return e;
   const PfdDMArgs d{a, chis};
   const char* g = getenv("PFE_GLM");
   const char* b = getenv("PFE_BLM");
   if (!(g && g[0] == '0') && !(b && b[0] == '0'))  // pooled group-LM unless an A/B run opts out
-    hipLaunchKernelGGL((k_pfd_dmfitg<2>), dim3((unsigned)a.pwaves), dim3(64), 0, st, d);
+    hipLaunchKernelGGL((k_pfd_dmfitg<2>), dim3((unsigned)a.pwaves), dim3(64), 0, sd, d);
   else
     hipLaunchKernelGGL((k_pfd_dmfitb<2, BLM_FPW>), dim3((unsigned)((n + a.fpw - 1) / a.fpw)),
-                       dim3(64), 0, st, d);
+                       dim3(64), 0, sd, d);
+  if ((e = launch_sine(a, st)) != hipSuccess) return e;
+  if (forked && (e = fork_end(fk, st)) != hipSuccess) return e;
   launch_clear_internal(status, n, st);
   return hipGetLastError();
 }
