@@ -56,10 +56,27 @@ static int persistent_waves(int64_t n) {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// workspace layout: [GaussWS x n][counters][per-wave scratch]
+// hand-over regions (lm_group.h HandOver) of the three chains: waves x slots x K x 16 lanes;
+// the Gaussian chain runs a.pwaves waves, the DM and sine kernels pool_grid(a, 3)
+static int64_t hand_waves(int64_t n, int region) {
+  const int64_t cap = (int64_t)device_cus() * (region == HAND_GAUSS ? 8 : 12);
+  return n < 1 ? 1 : n < cap ? n : cap;
+}
+static size_t hand_bytes(int64_t n, int region) {
+  const int k = region == HAND_GAUSS ? HAND_K_GAUSS : region == HAND_DM ? HAND_K_DM : HAND_K_SINE;
+  return (size_t)hand_waves(n, region) * GLM_FPW * k * 16 * sizeof(double);
+}
+static bool hand_on() {
+  const char* e = getenv("PFE_HAND");
+  return !(e && e[0] == '0');
+}
+
+// workspace layout: [GaussWS x n][counters][hand-over regions][per-wave scratch]
 size_t bates22_workspace_bytes(const pfe_bates_in* in) {
+  size_t hb = 0;
+  for (int r = 0; r < 3; ++r) hb += align256(hand_bytes(in->n, r));
   return 256 + align256((size_t)in->n * sizeof(GaussWS)) +
-         align256(BATES_NCOUNTERS * sizeof(unsigned)) +
+         align256(BATES_NCOUNTERS * sizeof(unsigned)) + hb +
          (size_t)persistent_waves(in->n) * gdg_wave_scratch_doubles(in->lp) * sizeof(double);
 }
 
@@ -81,6 +98,11 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
   wb += align256((size_t)n * sizeof(GaussWS));
   a.counters = (unsigned*)wb;
   wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
+  const bool ho = hand_on();
+  for (int r = 0; r < 3; ++r) {
+    a.hand[r] = ho ? (double*)wb : nullptr;
+    wb += align256(hand_bytes(n, r));
+  }
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());

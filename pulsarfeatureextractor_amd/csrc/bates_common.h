@@ -55,9 +55,15 @@ struct BatesArgs {
                        // use fewer so that there are several waves per wave slot
   int gslots;          // fit slots per wave of the pooled kernels (<= GLM_FPW)
   int cus;             // compute units of the device
+  double* hand[3];     // hand-over scratch of the pooled kernels per stream (HAND_*), or null
 };
 
 constexpr int BATES_NCOUNTERS = 16;
+// Hand-over scratch (lm_group.h HandOver): one region per concurrently running chain, sized
+// for HAND_K doubles per group lane per slot (residuals + cached model terms) and up to
+// hand_waves() waves; a kernel whose functor needs more re-evaluates instead.
+enum : int { HAND_GAUSS = 0, HAND_DM = 1, HAND_SINE = 2 };
+constexpr int HAND_K_GAUSS = 24, HAND_K_DM = 24, HAND_K_SINE = 8;
 
 // Side streams of a handle: the score groups that do not depend on each other run on them
 // concurrently with the caller's stream (sine fits | Gaussian chain | DM fit + sub-bands), so

@@ -746,7 +746,7 @@ __global__ __launch_bounds__(64, 2) void k_ghistg(BatesArgs a) {
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   GhistProb<P, F, FPW> prob{a, T, HS, cnt, hist, stage, a.gslots};
-  glm_engine<3, 4, FPW>(prob, S, T.ph, T.list);
+  glm_engine<3, 4, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 template <int P, bool F, int FPW>
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(64, 2) void k_gfixg(BatesArgs a) {
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   GfixProb<P, F, FPW> prob{a, T, cnt, hist, a.gslots};
-  glm_engine<2, 4, FPW>(prob, S, T.ph, T.list);
+  glm_engine<2, 4, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1746,7 +1746,7 @@ __global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   Gt1Prob<P, FPW> prob{a, T, a.gslots};
-  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
+  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the 8 peel passes ----------------------------------------------------------
@@ -1869,7 +1869,7 @@ __global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
   double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   double* yv = xs + (size_t)FPW * 64 * P;
   PeelProb<P, FPW> prob{a, T, xs, yv, ys, cx, a.gslots};
-  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list);
+  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the final 8-parameter fit ----------------------------------------------
@@ -1934,7 +1934,7 @@ __global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   Gdg8Prob<P, FPW> prob{a, T, a.gslots};
-  glm_engine<8, 4 * P, FPW>(prob, S, T.ph, T.list);
+  glm_engine<8, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- launchers -----------------------------------------------------------------------

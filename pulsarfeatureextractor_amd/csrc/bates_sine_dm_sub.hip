@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64, 3) void k_sineg(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   SineProb<MPL, F, FPW> prob{a, T, stage, a.gslots};
-  glm_engine<2, 4 * MPL, FPW>(prob, S, T.ph, T.list);
+  glm_engine<2, 4 * MPL, FPW>(prob, S, T.ph, T.list, a.hand[HAND_SINE], HAND_K_SINE);
 }
 
 // ======================================================================================
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(64, 3) void k_dmfitg(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   DMProb<MPL, FPW> prob{a, T, a.gslots};
-  glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list);
+  glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list, a.hand[HAND_DM], HAND_K_DM);
 }
 
 // ======================================================================================

@@ -25,6 +25,8 @@
 // in that summation order (last-bit), i.e. like any other non-sequential lmdif.
 #pragma once
 
+#include <type_traits>
+
 #include "lm_batch.h"
 
 namespace pfe {
@@ -198,20 +200,59 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
   }
 }
 
+// Hand-over of an accepted trial's residuals (and the functor's cached terms, e.g. the exp
+// factors) to the slot's next O-phase, through per-wave global scratch laid out
+// [slot][word][group lane]: MINPACK's fvec = wa4 after a successful step, instead of
+// evaluating the function at the new x once more.  nullptr: re-evaluate (same bits).
+template <int MPL, class Fn>
+struct HandOver {
+  using Cache = typename FnCache<Fn>::type;
+  static constexpr int CW = HasCols<Fn>::value ? (int)(sizeof(Cache) / sizeof(double)) : 0;
+  static constexpr int K = MPL + CW;  // doubles per group lane per slot
+  __device__ static __forceinline__ void put(double* hand, int f, const double (&fv)[MPL],
+                                             const Cache& c) {
+    double* h = hand + (size_t)f * K * GLM_G + glane();
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) h[k * GLM_G] = fv[k];
+    if constexpr (CW > 0) {
+      double w[CW > 0 ? CW : 1];
+      __builtin_memcpy(w, &c, sizeof(Cache));
+#pragma unroll
+      for (int i = 0; i < CW; ++i) h[(MPL + i) * GLM_G] = w[i];
+    }
+  }
+  __device__ static __forceinline__ void get(const double* hand, int f, double (&fv)[MPL],
+                                             Cache& c) {
+    const double* h = hand + (size_t)f * K * GLM_G + glane();
+#pragma unroll
+    for (int k = 0; k < MPL; ++k) fv[k] = h[k * GLM_G];
+    if constexpr (CW > 0) {
+      double w[CW > 0 ? CW : 1];
+#pragma unroll
+      for (int i = 0; i < CW; ++i) w[i] = h[(MPL + i) * GLM_G];
+      __builtin_memcpy(&c, w, sizeof(Cache));
+    }
+  }
+};
+
 // O-phase for slot f (one group): residuals at S.x (a fresh fit also initialises par, delta,
 // xnorm, the counters and fnorm), the forward-difference Jacobian, QR, Q^T f, R -> LDS.
 // Leaves info = -1 (the gtol test runs in the next SIMT phase).
 template <int N, int MPL, int FPW, class Fn>
-__device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>& S, bool fresh) {
+__device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>& S, bool fresh,
+                                          const double* hand) {
   const double eps = 1.4901161193847656e-08;  // sqrt(max(epsfcn, epsmch)) = 2^-26
   const int gl = glane();
   double x[N], fvec[MPL];
   typename FnCache<Fn>::type cache;
 #pragma unroll
   for (int j = 0; j < N; ++j) x[j] = S.x[j][f];
-  // the residuals at x: for an accepted step these are the trial's residuals, recomputed
-  // (same function, same operands: the same bits)
-  fn_eval<Fn, N, MPL>(fcn, x, fvec, cache);
+  // the residuals at x: for an accepted step the trial's residuals, handed over or
+  // recomputed (same function, same operands: the same bits)
+  if (!fresh && hand)
+    HandOver<MPL, Fn>::get(hand, f, fvec, cache);
+  else
+    fn_eval<Fn, N, MPL>(fcn, x, fvec, cache);
   int iter, nfev;
   double fnorm;
   if (fresh) {
@@ -303,7 +344,8 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
 // T-phase for slot f (one group): evaluate the trial point, update delta/par, accept or
 // reject, convergence tests.  Returns the slot's next phase.
 template <int N, int MPL, int FPW, class Fn>
-__device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>& S, int maxfev) {
+__device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>& S, int maxfev,
+                                         double* hand) {
   const int gl = glane();
   double wa2[N], wa4[MPL];
   typename FnCache<Fn>::type cache;
@@ -354,6 +396,7 @@ __device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>&
     if (delta <= EPSMCH * xnorm) info = 7;
     if (gnorm <= EPSMCH) info = 8;
   }
+  if (hand && accepted && info == 0) HandOver<MPL, Fn>::put(hand, f, wa4, cache);
   if (gl == 0) {
     S.delta[f] = delta;
     S.par[f] = par;
@@ -411,11 +454,18 @@ __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body&
 //                              false when the slot stays empty (work exhausted)
 //   Fn   load(int f) const  -- (one group) the residual functor of slot f, rows r = gl + 16k
 //   int  maxfev(int f) const
-// ph / list: LDS int[FPW] each.
+// ph / list: LDS int[FPW] each.  hand_region: hand-over scratch of FPW x hand_k x GLM_G
+// doubles per wave (block), or nullptr.
 template <int N, int MPL, int FPW, class Prob>
-__device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list) {
+__device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list,
+                                           double* hand_region = nullptr, int hand_k = 0) {
   static_assert(FPW <= 64, "one slot per lane in the SIMT phase");
   const int lane = lane_id();
+  using Fn = std::decay_t<decltype(prob.load(0))>;
+  constexpr int HK = HandOver<MPL, Fn>::K;
+  double* const hand = (hand_region && HK <= hand_k)
+                           ? hand_region + (size_t)blockIdx.x * FPW * hand_k * GLM_G
+                           : nullptr;
   if (lane < FPW) ph[lane] = PH_DONE;  // every slot takes its first fit in the refill step
   blm_sync();
 #ifdef PFE_LM_PROFILE
@@ -449,7 +499,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     if (mo) {
       glm_rounds(mo, list, [&](int f) {
         const auto fn = prob.load(f);
-        glm_outer<N, MPL, FPW>(fn, f, S, ph[f] == PH_INIT);
+        glm_outer<N, MPL, FPW>(fn, f, S, ph[f] == PH_INIT, hand);
       });
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
       blm_sync();
@@ -477,9 +527,11 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     if (mt) {
       glm_rounds(mt, list, [&](int f) {
         const auto fn = prob.load(f);
-        const int nph = glm_trial<N, MPL, FPW>(fn, f, S, prob.maxfev(f));
+        const int nph = glm_trial<N, MPL, FPW>(fn, f, S, prob.maxfev(f), hand);
         if (glane() == 0) ph[f] = nph;
       });
+      // slots change groups between phases: the hand-over stores precede the next loads
+      if (hand) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
 #ifdef PFE_LM_PROFILE
     c_t += lm_clock() - t0;
