@@ -103,6 +103,22 @@ def test_batched_solver_bit_identical(engine, monkeypatch):
     assert np.array_equal(np.nan_to_num(o0, nan=7.0), np.nan_to_num(o1, nan=7.0))
 
 
+def test_concurrent_groups_and_hand_over_bit_identical(engine, monkeypatch):
+    """The score groups on side streams (default) vs in order on one stream (PFE_SERIAL=1),
+    and the LM hand-over of accepted residuals (default) vs re-evaluation (PFE_HAND=0): the
+    same bits (tests/test_pfd22_gpu.py checks the PFD path)."""
+    b = bates_batch(300, seed=33)
+    ref = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    for env in ({"PFE_SERIAL": "1"}, {"PFE_HAND": "0"}, {"PFE_SERIAL": "1", "PFE_HAND": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        o, s = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+        for k in env:
+            monkeypatch.delenv(k)
+        assert np.array_equal(s, ref[1]), env
+        assert np.array_equal(np.nan_to_num(o, nan=7.0), np.nan_to_num(ref[0], nan=7.0)), env
+
+
 def test_device_pointers_and_determinism(engine):
     import torch
 
