@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-multicore", action="store_true",
+                    help="skip the multi-process CPU baseline of the 22-score paths")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL all-gather that reassembles the feature matrix")
     return ap.parse_args()
@@ -147,6 +149,26 @@ def cpu_baseline_bates22(lp, sample):
         "sample": f"{sample} synthetic config-3 candidates ({lp}-bin profile, 16x{lp} sub-bands, "
                   f"128-point DM curve) through the reference-equivalent numpy/scipy.optimize."
                   f"leastsq restatement (oracle.bates.bates22), {dt:.1f} s on 1 host core",
+    }
+
+
+def cpu_baseline_bates22_mp(lp, per_worker=300):
+    """SURVEY.md §8(d)(i) on all host cores: the same restatement in `workers` spawned
+    processes (16 on the GPU box's CPU share), per_worker candidates each."""
+    from oracle.bates_mp import bates22_multicore
+    from pulsarfeatureextractor_amd.synth import bates_batch
+
+    workers = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    n = workers * per_worker
+    b = bates_batch(n, lp=lp, lsb=lp, seed=4245)
+    dt = bates22_multicore(b["prof"], b["sub"], b["dmcurve"], b["scal"], workers)
+    return {
+        "value": n / dt,
+        "unit": "candidates/sec",
+        "cores": workers,
+        "kind": "port",
+        "sample": f"{n} synthetic config-3 candidates through oracle.bates.bates22 in {workers} "
+                  f"spawned processes (one BLAS thread each), {dt:.1f} s wall",
     }
 
 
@@ -539,6 +561,8 @@ def main():
                                                 f"combined per-candidate time"}
         else:
             result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
+        if args.path in ("bates22", "all30") and not args.no_cpu_multicore:
+            result["cpu_baseline_multicore"] = cpu_baseline_bates22_mp(args.lp)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
