@@ -23,6 +23,9 @@
  *     device (HBM) pointers and the call is asynchronous on the handle's stream (no host
  *     sync); without it they are host pointers and the library stages them through
  *     per-handle device scratch, returning when the outputs are back on the host.
+ *   - The 22-score calls run their independent score groups on two side streams the handle
+ *     owns; they start after the work already queued on the handle's stream and are joined
+ *     back into it (events) before the call returns, so callers only ever see one stream.
  *   - Raw IEEE values are returned (NaN/inf included).  NaN/inf -> "0" replacement is the
  *     writer's job, as in DataProcessor.storeScore (DataProcessor.py:321-325).
  *   - Return value: 0 = OK, otherwise a PFE_E* code; the text is in pfe_last_error().
