@@ -5,7 +5,7 @@ metric (BASELINE.json): candidates/sec of the 8-feature (Lyon) path on synthetic
 profile + 128-bin DM rows, plus HBM GB/s vs peak.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS_PER_GPU]
-                  [--path lyon8|bates22|pfd|pfd22]
+                  [--path lyon8|bates22|subband|all30|pfd|pfd22] [--option NAME=VALUE ...]
 
 One "step" = one pass of the hot path (pfe_lyon8_u8 through the C-ABI, device pointers,
 inputs resident in HBM) over the rank's whole batch of synthetic candidates (config 2:
@@ -22,6 +22,13 @@ Besides the contract fields the JSON line carries:
   cpu_baseline : the reference-equivalent per-candidate numpy/scipy loop (oracle.lyon.lyon8,
                  the scalar port of PHCXFile.py:320-379) timed on this host, 1 core, on a
                  bounded sample of the same synthetic rows (rank 0, N=1 only)
+  extra        : (default run, N=1 only; --no-extra skips it) the other BASELINE configs,
+                 each with its own roofline and CPU baseline:
+                   config3 -- pfe_bates22 over 10M resident config-3 candidates
+                   config4 -- pfe_subband3 over 1M candidates of 16 x 256 sub-bands
+                   config2_e2e -- config 2 end to end from pinned host memory (PCIe H2D of
+                                  the rows + kernel + D2H of the features, pipelined), with
+                                  the measured H2D bandwidth of the box
 """
 from __future__ import annotations
 
@@ -34,8 +41,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-FP64_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (counts an FMA as 2 operations)
+# -ffp-contract=off (parity with numpy's individually rounded operations): no FMA is issued,
+# so one operation per lane per cycle is the attainable VALU ceiling
+FP64_NOFMA_TOPS = 39.3
 
 
 def parse():
@@ -44,20 +54,25 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=None,
-                    help="candidates per GPU (default 10M for lyon8, 1M for bates22)")
-    ap.add_argument("--lp", type=int, default=128)
+                    help="candidates per GPU (default 10M lyon8 / bates22-at-10M via extra, "
+                         "1M bates22 / subband / all30)")
+    ap.add_argument("--lp", type=int, default=None)
     ap.add_argument("--ld", type=int, default=128)
-    ap.add_argument("--path", choices=["lyon8", "bates22", "all30", "pfd", "pfd22"], default="lyon8",
+    ap.add_argument("--path", choices=["lyon8", "bates22", "subband", "all30", "pfd", "pfd22"],
+                    default="lyon8",
                     help="all30: config 5's 8 Lyon features + 22 Bates scores per candidate "
-                         "into one (n, 30) feature matrix")
+                         "into one (n, 30) feature matrix; subband: config 4 (scores 20-22)")
     ap.add_argument("--pfd-shape", default="16x32x128", help="npart x nsub x proflen (pfd path)")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="rows for the CPU baseline sample (default 8000 lyon8 / 300 bates22; 0 disables)")
+                    help="rows for the CPU baseline sample (0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-multicore", action="store_true",
                     help="skip the multi-process CPU baseline of the 22-score paths")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra configs (N=1 lyon8)")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL all-gather that reassembles the feature matrix")
+    ap.add_argument("--option", action="append", default=[],
+                    help="handle option NAME=VALUE (pfe_set_option; A/B runs)")
     return ap.parse_args()
 
 
@@ -74,15 +89,23 @@ def load_traffic(name: str):
         return None
 
 
+def load_ops_per_candidate():
+    p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["ops_per_candidate"]
+    except Exception:
+        return None
+
+
+# ---- CPU baselines (oracle restatements: test infrastructure, timed beside the GPU) --------
 def cpu_baseline_lyon8(lp, ld, sample):
-    import numpy as np
+    import warnings
 
     from oracle.lyon import lyon8
     from pulsarfeatureextractor_amd.synth import lyon_batch
 
     prof, dm = lyon_batch(sample, lp, ld, seed=4242)
-    import warnings
-
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         lyon8(prof[:50], dm[:50])  # warm imports
@@ -90,13 +113,13 @@ def cpu_baseline_lyon8(lp, ld, sample):
         lyon8(prof, dm)
         dt = time.perf_counter() - t0
     return {
-        "value": sample / dt,
-        "unit": "candidates/sec",
-        "cores": 1,
-        "kind": "port",
+        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
         "sample": f"{sample} synthetic {lp}-bin profile + {ld}-bin DM rows through the "
                   f"reference-equivalent per-candidate numpy.mean/std + scipy.stats.skew/"
                   f"kurtosis loop (oracle.lyon.lyon8), {dt:.1f} s on 1 host core",
+        "note": "the per-candidate statistics only: the reference's own path also parses each "
+                "PHCX file (SURVEY.md §8(d) measured 736 candidates/s through its objects), so "
+                "this baseline is the faster of the two",
     }
 
 
@@ -118,10 +141,7 @@ def cpu_baseline_lyon8_omp(lp, ld, sample=2_000_000):
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     return {
-        "value": sample / best,
-        "unit": "candidates/sec",
-        "cores": threads,
-        "kind": "port",
+        "value": sample / best, "unit": "candidates/sec", "cores": threads, "kind": "port",
         "sample": f"{sample} synthetic {lp}-bin profile + {ld}-bin DM rows through the C "
                   f"restatement (oracle/c/lyon8_omp.c, two-pass float64 moments), best of 3, "
                   f"{best * 1e3:.0f} ms on {threads} OpenMP threads",
@@ -142,10 +162,7 @@ def cpu_baseline_bates22(lp, sample):
         bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
         dt = time.perf_counter() - t0
     return {
-        "value": sample / dt,
-        "unit": "candidates/sec",
-        "cores": 1,
-        "kind": "port",
+        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
         "sample": f"{sample} synthetic config-3 candidates ({lp}-bin profile, 16x{lp} sub-bands, "
                   f"128-point DM curve) through the reference-equivalent numpy/scipy.optimize."
                   f"leastsq restatement (oracle.bates.bates22), {dt:.1f} s on 1 host core",
@@ -163,12 +180,37 @@ def cpu_baseline_bates22_mp(lp, per_worker=300):
     b = bates_batch(n, lp=lp, lsb=lp, seed=4245)
     dt = bates22_multicore(b["prof"], b["sub"], b["dmcurve"], b["scal"], workers)
     return {
-        "value": n / dt,
-        "unit": "candidates/sec",
-        "cores": workers,
-        "kind": "port",
+        "value": n / dt, "unit": "candidates/sec", "cores": workers, "kind": "port",
         "sample": f"{n} synthetic config-3 candidates through oracle.bates.bates22 in {workers} "
                   f"spawned processes (one BLAS thread each), {dt:.1f} s wall",
+    }
+
+
+def cpu_baseline_subband(lsb, sample):
+    import warnings
+
+    import numpy as np
+
+    from oracle.bates import subband_scores
+    from pulsarfeatureextractor_amd.synth import bates_batch
+
+    b = bates_batch(sample, lp=lsb, lsb=lsb, seed=4246)
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        t0 = time.perf_counter()
+        for i in range(sample):
+            try:
+                subband_scores(b["sub"][i].astype(np.int64), b["prof"][i].astype(np.int64),
+                               float(b["scal"][i, 3]))
+            except Exception:
+                pass
+        dt = time.perf_counter() - t0
+    return {
+        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
+        "sample": f"{sample} synthetic candidates of 16x{lsb} sub-bands + {lsb}-bin profile "
+                  f"through the reference-equivalent getSubband_scores + getProfileCorr "
+                  f"restatement (oracle.bates.subband_scores: Python boxcar loops, numpy."
+                  f"corrcoef per pair), {dt:.1f} s on 1 host core",
     }
 
 
@@ -241,333 +283,471 @@ def cpu_baseline_pfd22(shape, sample):
     }
 
 
-def load_ops_per_candidate():
-    p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
-    try:
-        with open(p) as f:
-            return json.load(f)["ops_per_candidate"]
-    except Exception:
-        return None
+# ---- timing -----------------------------------------------------------------------------
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={self.world}", file=sys.stderr)
+        # PFE_BENCH_BACKEND=gloo (rehearsal only): N ranks sharing the GPUs there are, the
+        # barrier / max-over-ranks reduction over gloo; the driver's runs use RCCL ("nccl")
+        self.backend = os.environ.get("PFE_BENCH_BACKEND", "nccl")
+        if self.backend != "nccl":
+            local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        self.local = local
+        self.dist_on = self.world > 1
+        if self.dist_on:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(self.backend)
+        from pulsarfeatureextractor_amd._native import Engine
+
+        self.eng = Engine(local)
+        for o in args.option:
+            k, v = o.split("=", 1)
+            self.eng.set_option(k, int(v) if v.lstrip("-").isdigit() else v)
+        self.stream = torch.cuda.Stream(device=local)  # the kernels' stream; events record on it
+        torch.cuda.set_stream(self.stream)
+        self.eng.set_stream(self.stream.cuda_stream)
+        self.dev = f"cuda:{local}"
+
+    def barrier(self):
+        if self.dist_on:
+            self.dist.barrier()
+
+    def time_steps(self, step, steps, warmup, warm=None):
+        """W untimed warmup steps (or `warm()`), then EXACTLY `steps` steps bracketed by
+        barrier + synchronize; returns (elapsed s max over ranks, mean event ms per step on
+        the kernels' stream, its max over ranks)."""
+        torch = self.torch
+        torch.cuda.synchronize()
+        if warm is not None:
+            warm()
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            evs[i][0].record(self.stream)
+            step()
+            evs[i][1].record(self.stream)
+        torch.cuda.synchronize()
+        self.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        kern_max = kern_ms
+        if self.dist_on:
+            t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=self.dev)
+            if self.backend == "nccl":
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            else:
+                tc = t.cpu()
+                self.dist.all_reduce(tc, op=self.dist.ReduceOp.MAX)
+                t = tc
+            elapsed, kern_max = float(t[0]), float(t[1])
+        return elapsed, kern_ms, kern_max
 
 
-def main():
-    args = parse()
-    if args.n is None:
-        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "all30": 1_000_000, "pfd": 32768,
-                  "pfd22": 32768}[args.path]
-    if args.cpu_sample is None:
-        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "all30": 300, "pfd": 200,
-                           "pfd22": 60}[args.path]
-    pfd_shape = tuple(int(v) for v in args.pfd_shape.split("x"))
-    import torch
-    import torch.distributed as dist
+def tile_bates(ctx, n, lp, seed, nsub=16, lsb=None):
+    """A 16384-candidate synthetic block (SURVEY.md §8(d) recipe), tiled to n rows in HBM."""
+    import numpy as np
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    # PFE_BENCH_BACKEND=gloo (rehearsal only): N ranks sharing the GPUs there are, the
-    # barrier / max-over-ranks reduction over gloo; the driver's runs use RCCL ("nccl")
-    backend = os.environ.get("PFE_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dist_on = world > 1
-    if dist_on:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    from pulsarfeatureextractor_amd.synth import bates_batch
 
-    from pulsarfeatureextractor_amd._native import Engine
-    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+    torch = ctx.torch
+    blk = min(16384, n)
+    base = bates_batch(blk, lp=lp, nsub=nsub, lsb=lsb or lp, seed=seed)
+    reps = (n + blk - 1) // blk
+    bt = {}
+    for k, v in base.items():
+        t = torch.from_numpy(np.ascontiguousarray(v)).to(ctx.dev)
+        bt[k] = t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
+    return bt
 
-    eng = Engine(local)
-    stream = torch.cuda.Stream(device=local)  # the kernel's stream; events record on it
-    torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
 
-    n = args.n
-    dev = f"cuda:{local}"
-    if args.path == "lyon8":
-        # rank-specific synthetic shard, resident in HBM before timing
-        prof, dm = lyon_batch_torch(n, args.lp, args.ld, seed=20261017 + rank, device=dev)
-        out = torch.empty((n, 8), dtype=torch.float64, device=dev)
-
-        def step():
-            eng.lyon8(prof, dm, out=out)
-    elif args.path in ("pfd", "pfd22"):
-        import numpy as np
-
-        from pulsarfeatureextractor_amd import pfd as _pfd
-
-        blk = 1024  # synthetic folds generated on the host, tiled to n rows in HBM
-        profs, subfreqs, pscal = _pfd.batch_inputs(pfd_block(blk, pfd_shape, 20261019 + rank))
-        reps = (n + blk - 1) // blk
-
-        def tile(a):
-            t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-            return t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
-
-        tp, tf, ts = tile(profs), tile(subfreqs), tile(pscal)
-        del profs
-
-        if args.path == "pfd":
-            def step():
-                eng.pfd_dmprof(tp, tf, ts, profile=False, chis=False, lyon8=True)
-        else:
-            out = torch.empty((n, 22), dtype=torch.float64, device=dev)
-            status = torch.empty((n,), dtype=torch.int32, device=dev)
-
-            def step():
-                eng.pfd_bates22(tp, tf, ts, out=out, status=status)
-    else:
-        import numpy as np
-
-        from pulsarfeatureextractor_amd.synth import bates_batch
-
-        # a 16384-candidate synthetic block (SURVEY.md §8(d) recipe), tiled to n rows in HBM
-        base = bates_batch(16384, lp=args.lp, lsb=args.lp, seed=20261018 + rank)
-        reps = (n + 16383) // 16384
-        bt = {}
-        for k, v in base.items():
-            t = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
-            bt[k] = t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
-        out = torch.empty((n, 22), dtype=torch.float64, device=dev)
-        status = torch.empty((n,), dtype=torch.int32, device=dev)
-
-        if args.path == "bates22":
-            def step():
-                eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out, status=status)
-        else:
-            # config 5: the profile of each candidate also feeds the Lyon features, with a
-            # 128-bin DM array per candidate; one (n, 30) feature matrix per step
-            _, dmrows = lyon_batch_torch(n, args.lp, args.ld, seed=20261020 + rank, device=dev)
-            o8 = torch.empty((n, 8), dtype=torch.float64, device=dev)
-            out = torch.empty((n, 30), dtype=torch.float64, device=dev)
-
-            def step():
-                eng.lyon8(bt["prof"], dmrows, out=o8)
-                eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out22,
-                            status=status)
-                out[:, :8].copy_(o8)
-                out[:, 8:].copy_(out22)
-
-            out22 = torch.empty((n, 22), dtype=torch.float64, device=dev)
-    torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # step-duration events on the kernels' own stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-
-    if dist_on:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        if backend == "nccl":
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        else:
-            tc = t.cpu()
-            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
-            t = tc
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
-
-    total_rows = n * world * args.steps
-    value = total_rows / elapsed
-    common = {
-        "value": value,
+def common_fields(ctx, n, steps, warmup, elapsed):
+    return {
+        "value": n * ctx.world * steps / elapsed,
         "unit": "candidates/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / args.steps,
+        "n_gpus": ctx.world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed * 1e3 / steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "data": "synthetic (SURVEY.md §8(d) recipe, generated on device)",
     }
-    if args.path == "lyon8":
-        bytes_per_launch = n * (args.lp + args.ld + 8 * 8)
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(f"lyon8_u8_{args.lp}x{args.ld}_n{n}_pmc.json")
-        result = {
-            "metric": "candidates/sec (8-feature path, 128-bin)",
-            **common,
-            "dtype": "u8->int64/f64",
-            "config": {
-                "workload": f"config 2: {n} synthetic candidates per GPU, {args.lp}-bin profile + "
-                            f"{args.ld}-bin DM, 8 Lyon moment features (pfe_lyon8_u8)",
-                "candidates_per_gpu": n,
-                "profile_bins": args.lp,
-                "dm_bins": args.ld,
-                "parallelism": f"candidate shards x{world}, no collective",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "pfe::lyon8_u8_fast3<128, 2>",
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "avg_kernel_ms": kern_ms,
-                "avg_kernel_ms_max_over_ranks": kern_ms_max,
-            },
-        }
-    elif args.path == "pfd":
-        npart, nsub, L = pfd_shape
-        bytes_per_launch = n * (npart * nsub * L * 8 + nsub * 8 + 8 * 8 + 8 * 8 + 4)
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        result = {
-            "metric": "candidates/sec (PFD dmprof path)",
-            **common,
-            "dtype": "f64 (DM-curve statistics f32, as numpy)",
-            "config": {
-                "workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x {nsub} "
-                            f"sub-bands x {L} bins): dedispersion, 0..255 profile, 100-DM "
-                            f"chi^2 curve, 8 Lyon features (pfe_pfd_dmprof)",
-                "candidates_per_gpu": n,
-                "fold_shape": list(pfd_shape),
-                "parallelism": f"candidate shards x{world}, no collective",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "kernel": "pfe::k_pfd_dmprof",
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "avg_kernel_ms": kern_ms,
-                "avg_kernel_ms_max_over_ranks": kern_ms_max,
-            },
-        }
-    elif args.path == "pfd22":
-        npart, nsub, L = pfd_shape
-        result = {
-            "metric": "candidates/sec (PFD 22-score path)",
-            **common,
-            "dtype": "f64",
-            "config": {
-                "workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x {nsub} "
-                            f"sub-bands x {L} bins): PFDFile.compute, 22 scores "
-                            f"(pfe_pfd_bates22)",
-                "candidates_per_gpu": n,
-                "fold_shape": list(pfd_shape),
-                "parallelism": f"candidate shards x{world}, no collective",
-            },
-            "roofline": {
-                "bound": "fp64-valu",
-                "achieved": None,
-                "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": None,
-                "traffic": None,
-                "note": "operation count of the PFD 22-score path not frozen yet; the "
-                        "fits are the 22-score path's (see --path bates22)",
-                "kernel": "pfe_pfd_bates22 (9 kernels, one step)",
-                "avg_step_ms": kern_ms,
-                "avg_step_ms_max_over_ranks": kern_ms_max,
-            },
-        }
-    else:
-        ops = load_ops_per_candidate()
-        achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
-        all30 = args.path == "all30"
-        result = {
-            "metric": ("candidates/sec (8+22-feature path, 128-bin)" if all30
-                       else "candidates/sec (22-score path, 128-bin)"),
-            **common,
-            "dtype": "f64",
-            "config": {
-                "workload": (f"config 5 shard: {n} synthetic candidates per GPU, {args.lp}-bin "
-                             f"profile + {args.ld}-bin DM array, 16x{args.lp} sub-bands, 128-point "
-                             f"DM curve, 8 Lyon + 22 Bates features into one (n, 30) matrix "
-                             f"(pfe_lyon8_u8 + pfe_bates22)") if all30 else
-                            (f"config 3 shape: {n} synthetic candidates per GPU, {args.lp}-bin "
-                             f"profile, 16x{args.lp} sub-bands, 128-point DM curve, 22 Bates "
-                             f"scores (pfe_bates22)"),
-                "candidates_per_gpu": n,
-                "profile_bins": args.lp,
-                "parallelism": f"candidate shards x{world}, no collective",
-            },
-            "roofline": {
-                "bound": "fp64-valu",
-                "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
-                "traffic": None,
-                "kernel": ("pfe_lyon8_u8 + pfe_bates22, one step" if all30
-                           else "pfe_bates22 (8 kernels, one step)"),
-                "algorithmic_ops_per_candidate": ops,
-                "avg_step_ms": kern_ms,
-                "avg_step_ms_max_over_ranks": kern_ms_max,
-            },
-        }
-    if args.gather and dist_on:
-        # the optional reassembly step (RCCL all-gather of the n*world x 8 fp64 matrix over
-        # xGMI), timed on its own, outside the headline step
-        from pulsarfeatureextractor_amd.distributed import gather_rows
 
-        gather_rows(out, n * world)
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
-        full = gather_rows(out, n * world)
-        torch.cuda.synchronize()
-        dist.barrier()
-        gms = (time.perf_counter() - g0) * 1e3
-        result["gather"] = {"ms": gms, "bytes_received_per_rank": int(full.numel() * 8 * (world - 1) / world),
-                            "collective": "all_gather_into_tensor (RCCL)"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
-        if args.path == "lyon8":
-            result["cpu_baseline"] = cpu_baseline_lyon8(args.lp, args.ld, args.cpu_sample)
-            omp = cpu_baseline_lyon8_omp(args.lp, args.ld)
+
+# ---- paths ------------------------------------------------------------------------------
+def run_lyon8(ctx, args, n, lp):
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    torch = ctx.torch
+    prof, dm = lyon_batch_torch(n, lp, args.ld, seed=20261017 + ctx.rank, device=ctx.dev)
+    out = torch.empty((n, 8), dtype=torch.float64, device=ctx.dev)
+
+    def step():
+        ctx.eng.lyon8(prof, dm, out=out)
+
+    elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+    bytes_per_launch = n * (lp + args.ld + 8 * 8)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(f"lyon8_u8_{lp}x{args.ld}_n{n}_pmc.json")
+    return {
+        "metric": "candidates/sec (8-feature path, 128-bin)",
+        **common_fields(ctx, n, args.steps, args.warmup, elapsed),
+        "dtype": "u8->int64/f64",
+        "config": {
+            "workload": f"config 2: {n} synthetic candidates per GPU, {lp}-bin profile + "
+                        f"{args.ld}-bin DM, 8 Lyon moment features (pfe_lyon8_u8)",
+            "candidates_per_gpu": n, "profile_bins": lp, "dm_bins": args.ld,
+            "parallelism": f"candidate shards x{ctx.world}, no collective",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": f"pfe::lyon8_u8_fast3<{lp}, 2>",
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
+        },
+    }, out
+
+
+def bates_roofline(n, kern_ms, kern_max, kernel):
+    ops = load_ops_per_candidate()
+    achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
+    return {
+        "bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+        "frac_nofma_valu": (achieved / FP64_NOFMA_TOPS) if achieved else None,
+        "nofma_valu_peak": FP64_NOFMA_TOPS,
+        "traffic": None, "kernel": kernel,
+        "algorithmic_ops_per_candidate": ops,
+        "note": "algorithmic fp64 operations (add/mul/div/sqrt/exp/sin = 1 each, "
+                "tools/bates_flops.py) per second; frac against the 78.6 TFLOP/s FMA peak and "
+                "frac_nofma_valu against the 39.3 Tops/s one-op-per-lane ceiling that applies "
+                "with -ffp-contract=off",
+        "avg_step_ms": kern_ms, "avg_step_ms_max_over_ranks": kern_max,
+    }
+
+
+def run_bates22(ctx, args, n, lp, steps, warmup, small_warm=False):
+    torch = ctx.torch
+    bt = tile_bates(ctx, n, lp, 20261018 + ctx.rank)
+    out = torch.empty((n, 22), dtype=torch.float64, device=ctx.dev)
+    status = torch.empty((n,), dtype=torch.int32, device=ctx.dev)
+
+    def step():
+        ctx.eng.bates22(bt["prof"], bt["sub"], bt["dmcurve"], bt["scal"], out=out, status=status)
+
+    warm = None
+    if small_warm:  # one pass over the first 1M rows instead of a full-size warmup step
+        m = min(n, 1_000_000)
+
+        def warm():
+            ctx.eng.bates22(bt["prof"][:m], bt["sub"][:m], bt["dmcurve"][:m], bt["scal"][:m],
+                            out=out[:m], status=status[:m])
+
+    elapsed, kern_ms, kern_max = ctx.time_steps(step, steps, warmup, warm)
+    res = {
+        "metric": "candidates/sec (22-score path, 128-bin)",
+        **common_fields(ctx, n, steps, warmup, elapsed),
+        "dtype": "f64",
+        "config": {
+            "workload": f"config 3: {n} synthetic candidates per GPU, {lp}-bin profile, "
+                        f"16x{lp} sub-bands, 128-point DM curve, 22 Bates scores (pfe_bates22)",
+            "candidates_per_gpu": n, "profile_bins": lp,
+            "parallelism": f"candidate shards x{ctx.world}, no collective",
+        },
+        "roofline": bates_roofline(n, kern_ms, kern_max, "pfe_bates22 (8 kernels, one step)"),
+    }
+    if small_warm:
+        res["warmup_note"] = "untimed warm-up: one pass over the first 1M rows"
+    return res, out
+
+
+def run_subband(ctx, args, n, lsb, steps, warmup):
+    torch = ctx.torch
+    bt = tile_bates(ctx, n, lsb, 20261021 + ctx.rank, nsub=16, lsb=lsb)
+    del bt["dmcurve"]
+    out = torch.empty((n, 3), dtype=torch.float64, device=ctx.dev)
+    status = torch.empty((n,), dtype=torch.int32, device=ctx.dev)
+
+    def step():
+        ctx.eng.subband3(bt["prof"], bt["sub"], bt["scal"], out=out, status=status)
+
+    elapsed, kern_ms, kern_max = ctx.time_steps(step, steps, warmup)
+    # one read of the profile, the sub-bands and the width, one write of 3 scores + status
+    per_cand = lsb + 16 * lsb + 8 + 3 * 8 + 4
+    achieved = per_cand * n / (kern_ms * 1e-3) / 1e9
+    return {
+        "metric": "candidates/sec (sub-band scores 20-22, 16 x 256 bins)",
+        **common_fields(ctx, n, steps, warmup, elapsed),
+        "dtype": "u8->int32/f64",
+        "config": {
+            "workload": f"config 4: {n} synthetic candidates per GPU, {lsb}-bin profile, 16x{lsb} "
+                        f"sub-bands, scores 20-22 (pfe_subband3)",
+            "candidates_per_gpu": n, "subband_bins": lsb, "nsub": 16,
+            "parallelism": f"candidate shards x{ctx.world}, no collective",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "pfe::k_subband2<4, uint16_t, 4>",
+            "algorithmic_bytes_per_candidate": per_cand,
+            "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
+        },
+    }, out
+
+
+def run_e2e(ctx, args, n, lp, steps=5):
+    """Config 2 end to end from pinned host memory: pfe_lyon8_u8 with host pointers (H2D of
+    the rows, the kernel, D2H of the features; chunked and pipelined in the library)."""
+    import numpy as np
+
+    from pulsarfeatureextractor_amd._native import host_empty
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    torch = ctx.torch
+    dprof, ddm = lyon_batch_torch(n, lp, args.ld, seed=20261022, device=ctx.dev)
+    hp, hd = host_empty((n, lp), np.uint8), host_empty((n, args.ld), np.uint8)
+    out = host_empty((n, 8), np.float64)
+    torch.from_numpy(hp).copy_(dprof)
+    torch.from_numpy(hd).copy_(ddm)
+    dev_out = ctx.eng.lyon8(dprof, ddm)
+    torch.cuda.synchronize()
+    ctx.eng.lyon8(hp, hd, out=out)  # warm (staging slots, copy streams)
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        ctx.eng.lyon8(hp, hd, out=out)
+        ts.append(time.perf_counter() - t0)
+    same = bool(np.array_equal(np.nan_to_num(out, nan=7.0),
+                               np.nan_to_num(dev_out.cpu().numpy(), nan=7.0)))
+    # the box's H2D rate for the same bytes: one pinned copy of the input rows
+    nb = n * (lp + args.ld)
+    src = torch.from_numpy(hp.reshape(-1)[: n * lp])
+    dst = torch.empty(n * lp, dtype=torch.uint8, device=ctx.dev)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = 3 * n * lp / (time.perf_counter() - t0) / 1e9
+    del dst, dprof, ddm
+    t = min(ts)
+    return {
+        "value": n / t, "unit": "candidates/sec",
+        "workload": f"config 2 end to end: {n} candidates in pinned host memory (pfe_host_alloc), "
+                    f"pfe_lyon8_u8 with host pointers: chunked H2D of the {lp}+{args.ld}-byte "
+                    f"rows, the kernel and D2H of the 64-byte feature rows, overlapped on three "
+                    f"streams",
+        "ms": t * 1e3, "steps": steps,
+        "input_gbs": nb / t / 1e9,
+        "h2d_gbs_measured": h2d,
+        "frac_of_h2d": nb / t / 1e9 / h2d,
+        "identical_to_device_path": same,
+    }
+
+
+def main():
+    args = parse()
+    lp_default = {"subband": 256}.get(args.path, 128)
+    lp = args.lp or lp_default
+    if args.n is None:
+        args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "subband": 1_000_000,
+                  "all30": 1_000_000, "pfd": 32768, "pfd22": 32768}[args.path]
+    if args.cpu_sample is None:
+        args.cpu_sample = {"lyon8": 8000, "bates22": 300, "subband": 200, "all30": 300,
+                           "pfd": 200, "pfd22": 60}[args.path]
+    pfd_shape = tuple(int(v) for v in args.pfd_shape.split("x"))
+    ctx = Ctx(args)
+    torch = ctx.torch
+    n = args.n
+    want_cpu = ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0
+
+    out = None
+    if args.path == "lyon8":
+        result, out = run_lyon8(ctx, args, n, lp)
+        if want_cpu:
+            result["cpu_baseline"] = cpu_baseline_lyon8(lp, args.ld, args.cpu_sample)
+            omp = cpu_baseline_lyon8_omp(lp, args.ld)
             if omp is not None:
                 result["cpu_baseline_multicore"] = omp
-        elif args.path == "pfd":
-            result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
-        elif args.path == "pfd22":
-            result["cpu_baseline"] = cpu_baseline_pfd22(pfd_shape, args.cpu_sample)
-        elif args.path == "all30":
-            b = cpu_baseline_bates22(args.lp, args.cpu_sample)
-            l8 = cpu_baseline_lyon8(args.lp, args.ld, 8000)
+        if ctx.world == 1 and not args.no_extra:
+            extra = {}
+            del out
+            out = None
+            torch.cuda.empty_cache()
+            # config 3 at the 10M rows BASELINE names: 2 timed steps of ~16 s
+            r3, o3 = run_bates22(ctx, args, 10_000_000, 128, steps=2, warmup=0, small_warm=True)
+            del o3
+            torch.cuda.empty_cache()
+            if not args.no_cpu_baseline:
+                r3["cpu_baseline"] = cpu_baseline_bates22(128, 300)
+                if not args.no_cpu_multicore:
+                    r3["cpu_baseline_multicore"] = cpu_baseline_bates22_mp(128)
+            extra["config3"] = r3
+            r4, o4 = run_subband(ctx, args, 1_000_000, 256, steps=20, warmup=3)
+            del o4
+            torch.cuda.empty_cache()
+            if not args.no_cpu_baseline:
+                r4["cpu_baseline"] = cpu_baseline_subband(256, 200)
+            extra["config4"] = r4
+            extra["config2_e2e"] = run_e2e(ctx, args, n, lp)
+            result["extra"] = extra
+    elif args.path == "bates22":
+        result, out = run_bates22(ctx, args, n, lp, args.steps, args.warmup)
+        if want_cpu:
+            result["cpu_baseline"] = cpu_baseline_bates22(lp, args.cpu_sample)
+            if not args.no_cpu_multicore:
+                result["cpu_baseline_multicore"] = cpu_baseline_bates22_mp(lp)
+    elif args.path == "subband":
+        result, out = run_subband(ctx, args, n, lp, args.steps, args.warmup)
+        if want_cpu:
+            result["cpu_baseline"] = cpu_baseline_subband(lp, args.cpu_sample)
+    elif args.path == "all30":
+        from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+        bt = tile_bates(ctx, n, lp, 20261018 + ctx.rank)
+        # config 5: the profile of each candidate also feeds the Lyon features, with a
+        # 128-bin DM array per candidate; one (n, 30) feature matrix per step
+        _, dmrows = lyon_batch_torch(n, lp, args.ld, seed=20261020 + ctx.rank, device=ctx.dev)
+        out = torch.empty((n, 30), dtype=torch.float64, device=ctx.dev)
+
+        def step():
+            ctx.eng.features30(bt["prof"], dmrows, bt["sub"], bt["dmcurve"], bt["scal"], out=out)
+
+        elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+        result = {
+            "metric": "candidates/sec (8+22-feature path, 128-bin)",
+            **common_fields(ctx, n, args.steps, args.warmup, elapsed),
+            "dtype": "f64",
+            "config": {
+                "workload": f"config 5 shard: {n} synthetic candidates per GPU, {lp}-bin profile "
+                            f"+ {args.ld}-bin DM array, 16x{lp} sub-bands, 128-point DM curve, 8 "
+                            f"Lyon + 22 Bates features into one (n, 30) matrix (Engine.features30: "
+                            f"pfe_lyon8_u8 + pfe_bates22)",
+                "candidates_per_gpu": n, "profile_bins": lp,
+                "parallelism": f"candidate shards x{ctx.world}, no collective",
+            },
+            "roofline": bates_roofline(n, kern_ms, kern_max, "pfe_lyon8_u8 + pfe_bates22, one step"),
+        }
+        if want_cpu:
+            b = cpu_baseline_bates22(lp, args.cpu_sample)
+            l8 = cpu_baseline_lyon8(lp, args.ld, 8000)
             v = 1.0 / (1.0 / b["value"] + 1.0 / l8["value"])
             result["cpu_baseline"] = {"value": v, "unit": "candidates/sec", "cores": 1,
                                       "kind": "port",
                                       "sample": f"{b['sample']}; plus {l8['sample']}; "
                                                 f"combined per-candidate time"}
+            if not args.no_cpu_multicore:
+                result["cpu_baseline_multicore"] = cpu_baseline_bates22_mp(lp)
+    else:
+        import numpy as np
+
+        from pulsarfeatureextractor_amd import pfd as _pfd
+
+        blk = 1024  # synthetic folds generated on the host, tiled to n rows in HBM
+        profs, subfreqs, pscal = _pfd.batch_inputs(pfd_block(blk, pfd_shape, 20261019 + ctx.rank))
+        reps = (n + blk - 1) // blk
+
+        def tile(a):
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+            return t.repeat((reps,) + (1,) * (t.dim() - 1))[:n].contiguous()
+
+        tp, tf, ts = tile(profs), tile(subfreqs), tile(pscal)
+        del profs
+        npart, nsub, L = pfd_shape
+        common_cfg = {"candidates_per_gpu": n, "fold_shape": list(pfd_shape),
+                      "parallelism": f"candidate shards x{ctx.world}, no collective"}
+        if args.path == "pfd":
+            holder = {}
+
+            def step():
+                holder["r"] = ctx.eng.pfd_dmprof(tp, tf, ts, profile=False, chis=False, lyon8=True)
+
+            elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+            out = holder["r"]["lyon8"]
+            bytes_per_launch = n * (npart * nsub * L * 8 + nsub * 8 + 8 * 8 + 8 * 8 + 4)
+            achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+            result = {
+                "metric": "candidates/sec (PFD dmprof path)",
+                **common_fields(ctx, n, args.steps, args.warmup, elapsed),
+                "dtype": "f64 (DM-curve statistics f32, as numpy)",
+                "config": {"workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x "
+                                       f"{nsub} sub-bands x {L} bins): dedispersion, 0..255 "
+                                       f"profile, 100-DM chi^2 curve, 8 Lyon features "
+                                       f"(pfe_pfd_dmprof)", **common_cfg},
+                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                             "kernel": "pfe::k_pfd_dmprof4",
+                             "algorithmic_bytes_per_launch": bytes_per_launch,
+                             "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max},
+            }
+            if want_cpu:
+                result["cpu_baseline"] = cpu_baseline_pfd(pfd_shape, args.cpu_sample)
         else:
-            result["cpu_baseline"] = cpu_baseline_bates22(args.lp, args.cpu_sample)
-        if args.path in ("bates22", "all30") and not args.no_cpu_multicore:
-            result["cpu_baseline_multicore"] = cpu_baseline_bates22_mp(args.lp)
-    if rank == 0:
+            out = torch.empty((n, 22), dtype=torch.float64, device=ctx.dev)
+            status = torch.empty((n,), dtype=torch.int32, device=ctx.dev)
+
+            def step():
+                ctx.eng.pfd_bates22(tp, tf, ts, out=out, status=status)
+
+            elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+            result = {
+                "metric": "candidates/sec (PFD 22-score path)",
+                **common_fields(ctx, n, args.steps, args.warmup, elapsed),
+                "dtype": "f64",
+                "config": {"workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x "
+                                       f"{nsub} sub-bands x {L} bins): PFDFile.compute, 22 scores "
+                                       f"(pfe_pfd_bates22)", **common_cfg},
+                "roofline": {"bound": "fp64-valu", "achieved": None, "peak": FP64_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": None, "traffic": None,
+                             "note": "operation count of the PFD 22-score path not frozen; the "
+                                     "fits are the 22-score path's (see --path bates22)",
+                             "kernel": "pfe_pfd_bates22 (9 kernels, one step)",
+                             "avg_step_ms": kern_ms, "avg_step_ms_max_over_ranks": kern_max},
+            }
+            if want_cpu:
+                result["cpu_baseline"] = cpu_baseline_pfd22(pfd_shape, args.cpu_sample)
+    if args.gather and ctx.dist_on and out is not None:
+        # the optional reassembly step (RCCL all-gather of the n*world x F fp64 matrix over
+        # xGMI), timed on its own, outside the headline step
+        from pulsarfeatureextractor_amd.distributed import gather_rows
+
+        gather_rows(out, n * ctx.world)
+        torch.cuda.synchronize()
+        ctx.barrier()
+        g0 = time.perf_counter()
+        full = gather_rows(out, n * ctx.world)
+        torch.cuda.synchronize()
+        ctx.barrier()
+        gms = (time.perf_counter() - g0) * 1e3
+        result["gather"] = {"ms": gms, "rows": int(full.shape[0]), "width": int(full.shape[1]),
+                            "bytes_received_per_rank": int(full.numel() * 8 * (ctx.world - 1) / ctx.world),
+                            "collective": "all_gather_into_tensor (RCCL)"}
+    if ctx.rank == 0:
         print(json.dumps(result), flush=True)
-    eng.close()
-    if dist_on:
-        dist.destroy_process_group()
+    ctx.eng.close()
+    if ctx.dist_on:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

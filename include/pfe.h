@@ -35,6 +35,7 @@
 #ifndef PFE_H_
 #define PFE_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -60,8 +61,8 @@ extern "C" {
 #define PFE_ST_DMFIT_FAIL     0x004u /* scores 16-19 raised          (PHCXFile.py:626-629) */
 #define PFE_ST_SUBBAND_FAIL   0x008u /* scores 20-22 raised          (PHCXFile.py:665-668) */
 #define PFE_ST_UNSUPPORTED    0x010u /* outside the shapes this build scores (a histogram with
-                                        more than 1024 Freedman-Diaconis bins, more than 16
-                                        sub-bands); the row is not scored */
+                                        more than 1024 Freedman-Diaconis bins); the row is not
+                                        scored */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu
@@ -87,6 +88,48 @@ const char* pfe_last_error(const pfe_handle* h);
 int pfe_set_stream(pfe_handle* h, void* hip_stream);
 /* Block until all work queued on the handle's stream has finished. */
 int pfe_synchronize(pfe_handle* h);
+
+/* ---------------------------------------------------------------------------------------
+ * Handle options (A/B and verification switches).  The defaults are the product
+ * configuration; the library never reads the process environment, so only an explicit
+ * pfe_set_option changes what a handle computes.  Options marked (bits) change the last
+ * bits of the LM-fitted scores (the m-sums are ordered differently); all others give
+ * identical results and only change the schedule.
+ *   PFE_OPT_SOLVER       (bits) LM solver of the 22-score kernels: PFE_SOLVER_POOLED
+ *                        (default; pooled 16-lane-group engine for <= 128 bins, batched
+ *                        beyond), PFE_SOLVER_BATCHED (one wave owns 32 fits), or
+ *                        PFE_SOLVER_WAVE (one wave per fit; bit-identical to BATCHED)
+ *   PFE_OPT_SERIAL       1: the independent score groups run in order on the handle's
+ *                        stream instead of on its two side streams (default 0)
+ *   PFE_OPT_HANDOVER     0: re-evaluate the residuals after an accepted LM step instead of
+ *                        handing the trial's residuals over (default 1)
+ *   PFE_OPT_GSLOTS       fit slots per pooled wave, 1..32 (0 = sized from n; default 0)
+ *   PFE_OPT_LYON8_BLOCKS grid cap of the Lyon-8 stream kernel (default 8192)
+ *   PFE_OPT_LYON8_BURST  candidate groups per wave step of the Lyon-8 kernel: 1, 2 or 4
+ *                        (default 2)
+ *   PFE_OPT_PFD_WAVES    waves per fold of the PFD preprocessing kernel: 4 (default) or 1
+ * Returns PFE_EINVAL for an unknown option or an out-of-range value.
+ * --------------------------------------------------------------------------------------- */
+#define PFE_OPT_SOLVER 1
+#define PFE_OPT_SERIAL 2
+#define PFE_OPT_HANDOVER 3
+#define PFE_OPT_GSLOTS 4
+#define PFE_OPT_LYON8_BLOCKS 5
+#define PFE_OPT_LYON8_BURST 6
+#define PFE_OPT_PFD_WAVES 7
+#define PFE_SOLVER_POOLED 0
+#define PFE_SOLVER_BATCHED 1
+#define PFE_SOLVER_WAVE 2
+int pfe_set_option(pfe_handle* h, int32_t option, int64_t value);
+int pfe_get_option(const pfe_handle* h, int32_t option, int64_t* value);
+
+/* Pinned (page-locked) host memory.  Host-pointer calls DMA pinned caller buffers in place
+ * (chunked, with the copies of one chunk overlapping the kernel of another); pageable
+ * buffers are staged through the handle's own pinned ring by the calling thread.  A
+ * producer that writes candidate rows straight into pfe_host_alloc memory (e.g.
+ * pfe_phcx_pack) therefore skips that staging copy.  Not tied to a handle. */
+int pfe_host_alloc(size_t bytes, void** out);
+void pfe_host_free(void* p);
 
 /* ---------------------------------------------------------------------------------------
  * 8 Lyon features.
@@ -145,6 +188,18 @@ typedef struct pfe_bates_in {
 
 int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
                 uint32_t flags);
+
+/* Sub-band scores alone (scores 20-22):
+ *   pfe_subband3 <- PHCXOperations.getSubbandParameters          PHCXOperations.py:305-349
+ *                   (getSubband_scores ProfileOperations.py:1585-1686, getProfileCorr
+ *                    PHCXOperations.py:387-415)
+ * Reads prof, sub and scal[PFE_SCAL_WIDTH] of `in` (dmcurve/ndm are ignored and may be
+ * NULL/0); out = n x 3 fp64 [RMS of sub-band peak positions, mean pairwise correlation,
+ * sum of profile correlations > 0.0055]; status bits PFE_ST_SUBBAND_FAIL where the
+ * reference raises (boxcar width <= 0 or > nBins, every pair NaN, lp != lsb).
+ * Any nsub in [2, 256] and lsb in [1, 1024] with nsub * (lsb + 1) <= 32768. */
+int pfe_subband3(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                 uint32_t flags);
 
 /* ---- PFD (PRESTO fold) files: preprocessing + Lyon features -------------------------
  * pfe_pfd_dmprof <- what a freshly loaded PFDFile computes for the dmprof path

@@ -23,6 +23,7 @@ PFE_ST_SINE_FAIL = 0x001
 PFE_ST_GAUSS_FAIL = 0x002
 PFE_ST_DMFIT_FAIL = 0x004
 PFE_ST_SUBBAND_FAIL = 0x008
+PFE_ST_UNSUPPORTED = 0x010
 PFE_ST_DGF_INDEXERROR = 0x100
 
 # every symbol include/pfe.h declares (checked by tests/test_capi_symbols.py)
@@ -34,9 +35,14 @@ EXPORTED_SYMBOLS = (
     "pfe_last_error",
     "pfe_set_stream",
     "pfe_synchronize",
+    "pfe_set_option",
+    "pfe_get_option",
+    "pfe_host_alloc",
+    "pfe_host_free",
     "pfe_lyon8_u8",
     "pfe_lyon8_f64",
     "pfe_bates22",
+    "pfe_subband3",
     "pfe_pfd_dmprof",
     "pfe_pfd_bates22",
 )
@@ -54,6 +60,19 @@ EXPORTED_IO_SYMBOLS = (
 )
 PFE_PHCX_PROFILE, PFE_PHCX_LYON_DM, PFE_PHCX_SUBBANDS, PFE_PHCX_DM_CURVE, PFE_PHCX_FIT_BLOCK = range(5)
 PFE_IO_STATUS = {0: "ok", 1: "open", 2: "gzip", 3: "xml", 4: "value", 5: "range", 6: "shape"}
+
+
+# handle options (include/pfe.h PFE_OPT_*): name -> (id, default)
+OPTIONS = {
+    "solver": 1,        # 0 pooled (default), 1 batched, 2 wave per fit
+    "serial": 2,
+    "handover": 3,
+    "gslots": 4,
+    "lyon8_blocks": 5,
+    "lyon8_burst": 6,
+    "pfd_waves": 7,
+}
+SOLVERS = {"pooled": 0, "batched": 1, "wave": 2}
 
 
 class PfeError(RuntimeError):
@@ -157,12 +176,22 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_set_stream.argtypes = [vp, vp]
         lib.pfe_synchronize.restype = C.c_int
         lib.pfe_synchronize.argtypes = [vp]
+        lib.pfe_set_option.restype = C.c_int
+        lib.pfe_set_option.argtypes = [vp, i32, i64]
+        lib.pfe_get_option.restype = C.c_int
+        lib.pfe_get_option.argtypes = [vp, i32, C.POINTER(i64)]
+        lib.pfe_host_alloc.restype = C.c_int
+        lib.pfe_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+        lib.pfe_host_free.restype = None
+        lib.pfe_host_free.argtypes = [vp]
         lib.pfe_lyon8_u8.restype = C.c_int
         lib.pfe_lyon8_u8.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
         lib.pfe_lyon8_f64.restype = C.c_int
         lib.pfe_lyon8_f64.argtypes = [vp, vp, i64, i32, vp, i64, i32, i64, vp, vp, u32]
         lib.pfe_bates22.restype = C.c_int
         lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
+        lib.pfe_subband3.restype = C.c_int
+        lib.pfe_subband3.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
         lib.pfe_pfd_dmprof.restype = C.c_int
         lib.pfe_pfd_dmprof.argtypes = [vp, C.POINTER(PfdIn), vp, vp, vp, vp, u32]
         lib.pfe_pfd_bates22.restype = C.c_int
@@ -198,12 +227,44 @@ def _is_device(a) -> bool:
     return bool(getattr(a, "is_cuda", False))
 
 
+class _Pinned:
+    """Owner of one pfe_host_alloc block; numpy arrays made by Engine.host_empty keep it
+    alive as their base and it is freed with the last of them."""
+
+    def __init__(self, lib, nbytes: int):
+        self.lib = lib
+        p = C.c_void_p()
+        if lib.pfe_host_alloc(max(1, int(nbytes)), C.byref(p)) != PFE_OK or not p.value:
+            raise MemoryError(f"pfe_host_alloc({nbytes}) failed")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.__array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1",
+                                    "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self.lib.pfe_host_free(self.ptr)
+            self.ptr = None
+
+
+def host_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """An uninitialised numpy array in pinned host memory (pfe_host_alloc): host-pointer
+    engine calls DMA such buffers in place instead of staging them."""
+    lib = load_library()
+    dt = np.dtype(dtype)
+    shape = tuple(int(v) for v in np.atleast_1d(shape))
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    raw = np.asarray(_Pinned(lib, nbytes))
+    return raw.view(dt).reshape(shape) if nbytes else np.empty(shape, dtype=dt)
+
+
 class Engine:
     """One libpfe handle: a GPU ordinal plus a HIP stream.
 
     Arguments may be numpy arrays (host; the call stages and synchronises) or torch CUDA
-    tensors (device; the call is asynchronous on the engine's stream).  Mixed placements
-    are rejected.
+    tensors (device; the call is asynchronous on torch's current stream).  Mixed placements
+    are rejected, and device tensors are checked for dtype, shape, contiguity and device
+    before any pointer reaches the library.
     """
 
     def __init__(self, device: int = 0):
@@ -247,10 +308,83 @@ class Engine:
         kernels that produced their inputs and before the ones that consume the outputs."""
         import torch
 
-        self.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def synchronize(self):
         self._check(self.lib.pfe_synchronize(self._h))
+
+    # -- options -------------------------------------------------------------------------
+    def set_option(self, name: str, value):
+        """pfe_set_option: name in OPTIONS ('solver' also takes 'pooled'/'batched'/'wave')."""
+        if name == "solver" and isinstance(value, str):
+            value = SOLVERS[value]
+        self._check(self.lib.pfe_set_option(self._h, OPTIONS[name], int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self._check(self.lib.pfe_get_option(self._h, OPTIONS[name], C.byref(v)))
+        return int(v.value)
+
+    def options(self, **kw):
+        """Context manager: set options for a block, restore the previous values after."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_option(k) for k in kw}
+            try:
+                for k, v in kw.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+
+        return cm()
+
+    # -- argument checks of the device path ----------------------------------------------
+    def _dev(self, t, name, dtypes, shape=None, rows_contig=False):
+        import torch
+
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise TypeError(f"{name}: expected a CUDA tensor (all arguments device or all host)")
+        if t.dtype not in dtypes:
+            raise TypeError(f"{name}: dtype {t.dtype}, expected one of {tuple(dtypes)}")
+        if t.device.index != self.device:
+            raise ValueError(f"{name}: on cuda:{t.device.index}, engine is on cuda:{self.device}")
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+        if rows_contig:
+            if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) < t.shape[1]:
+                raise ValueError(f"{name}: rows must be contiguous (stride(1) == 1)")
+        elif not t.is_contiguous():
+            raise ValueError(f"{name}: device tensors must be contiguous")
+        return t
+
+    def _status_dev(self, status, n):
+        import torch
+
+        if status is None:
+            return torch.empty((n,), dtype=torch.int32, device=f"cuda:{self.device}")
+        return self._dev(status, "status", (torch.int32,), (n,))
+
+    @staticmethod
+    def _status_host(status, n):
+        if status is None:
+            return np.empty((n,), dtype=np.uint32)
+        if not isinstance(status, np.ndarray) or status.dtype.itemsize != 4 or \
+                status.dtype.kind not in "iu" or status.shape != (n,) or not status.flags.c_contiguous:
+            raise ValueError("status must be a contiguous (n,) 4-byte integer array")
+        return status
+
+    @staticmethod
+    def _out_host(out, n, width):
+        if out is None:
+            return np.empty((n, width), dtype=np.float64)
+        if not isinstance(out, np.ndarray) or out.dtype != np.float64 or out.shape != (n, width) \
+                or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a contiguous ({n}, {width}) float64 array")
+        return out
 
     # -- 8 Lyon features -----------------------------------------------------------------
     def lyon8(self, prof, dm, out=None, status=None):
@@ -264,20 +398,18 @@ class Engine:
         if dev:
             import torch
 
+            self._dev(prof, "prof", (torch.uint8, torch.float64), rows_contig=True)
+            self._dev(dm, "dm", (prof.dtype,), rows_contig=True)
+            kind = "u8" if prof.dtype == torch.uint8 else "f64"
             self._follow_torch()
             if out is None:
                 out = torch.empty((n, 8), dtype=torch.float64, device=prof.device)
-            dtype_ok = {torch.uint8: "u8", torch.float64: "f64"}
-            kind = dtype_ok.get(prof.dtype)
-            if kind is None or dm.dtype != prof.dtype:
-                raise TypeError("lyon8: rows must be uint8 or float64 (same dtype)")
+            self._dev(out, "out", (torch.float64,), (n, 8))
+            if status is not None:
+                self._status_dev(status, n)
             ps, ds = prof.stride(0), dm.stride(0)
-            if prof.stride(1) != 1 or dm.stride(1) != 1 or not out.is_contiguous():
-                raise ValueError("lyon8: rows must be contiguous")
             flags = PFE_FLAG_DEVICE_PTRS
         else:
-            if out is None:
-                out = np.empty((n, 8), dtype=np.float64)
             if prof.dtype == np.uint8 and dm.dtype == np.uint8:
                 kind = "u8"
             elif prof.dtype == np.float64 and dm.dtype == np.float64:
@@ -287,8 +419,9 @@ class Engine:
             prof = prof if prof.strides[1] == prof.itemsize else np.ascontiguousarray(prof)
             dm = dm if dm.strides[1] == dm.itemsize else np.ascontiguousarray(dm)
             ps, ds = prof.strides[0] // prof.itemsize, dm.strides[0] // dm.itemsize
-            if out.dtype != np.float64 or not out.flags.c_contiguous or out.shape != (n, 8):
-                raise ValueError("lyon8: out must be a contiguous (n, 8) float64 array")
+            out = self._out_host(out, n, 8)
+            if status is not None:
+                self._status_host(status, n)
             flags = 0
         fn = self.lib.pfe_lyon8_u8 if kind == "u8" else self.lib.pfe_lyon8_f64
         st = None if status is None else _ptr(status)
@@ -298,67 +431,137 @@ class Engine:
         )
         return out
 
-    # -- 22 Bates scores -----------------------------------------------------------------
-    def bates22(self, prof, sub, dmcurve, scal, out=None, status=None):
-        """22 scores per candidate -> ((n, 22) float64, (n,) uint32 status)."""
+    # -- 22 Bates scores / sub-band scores -----------------------------------------------
+    def _bates_args(self, prof, sub, dmcurve, scal, with_dm):
         n = prof.shape[0]
-        if sub.shape[0] != n or dmcurve.shape[0] != n or scal.shape[0] != n:
-            raise ValueError("bates22: inputs must have the same number of rows")
-        if sub.ndim != 3 or scal.shape[1] != PFE_NSCAL:
-            raise ValueError("bates22: sub must be (n,nsub,lsb), scal (n,%d)" % PFE_NSCAL)
+        if prof.ndim != 2 or sub.ndim != 3 or scal.ndim != 2 or scal.shape[1] != PFE_NSCAL:
+            raise ValueError("prof must be (n,lp), sub (n,nsub,lsb), scal (n,%d)" % PFE_NSCAL)
+        if sub.shape[0] != n or scal.shape[0] != n or (with_dm and dmcurve.shape[0] != n):
+            raise ValueError("inputs must have the same number of rows")
+        if with_dm and dmcurve.ndim != 2:
+            raise ValueError("dmcurve must be (n, ndm)")
         dev = _is_device(prof)
         if dev:
             import torch
 
+            self._dev(prof, "prof", (torch.uint8,))
+            self._dev(sub, "sub", (torch.uint8,))
+            self._dev(scal, "scal", (torch.float64,))
+            if with_dm:
+                self._dev(dmcurve, "dmcurve", (torch.float64,))
             self._follow_torch()
-            if out is None:
-                out = torch.empty((n, 22), dtype=torch.float64, device=prof.device)
-            if status is None:
-                status = torch.empty((n,), dtype=torch.int32, device=prof.device)
-            for t in (prof, sub, dmcurve, scal, out, status):
-                if not t.is_contiguous():
-                    raise ValueError("bates22: device tensors must be contiguous")
-            flags = PFE_FLAG_DEVICE_PTRS
         else:
             prof = np.ascontiguousarray(prof, dtype=np.uint8)
             sub = np.ascontiguousarray(sub, dtype=np.uint8)
-            dmcurve = np.ascontiguousarray(dmcurve, dtype=np.float64)
             scal = np.ascontiguousarray(scal, dtype=np.float64)
-            if out is None:
-                out = np.empty((n, 22), dtype=np.float64)
-            if status is None:
-                status = np.empty((n,), dtype=np.uint32)
-            flags = 0
+            if with_dm:
+                dmcurve = np.ascontiguousarray(dmcurve, dtype=np.float64)
         bi = BatesIn(
             _ptr(prof), prof.shape[1], _ptr(sub), sub.shape[1], sub.shape[2],
-            _ptr(dmcurve), dmcurve.shape[1], _ptr(scal), n,
+            _ptr(dmcurve) if with_dm else None, dmcurve.shape[1] if with_dm else 0,
+            _ptr(scal), n,
         )
+        return bi, dev, (prof, sub, dmcurve, scal)
+
+    def bates22(self, prof, sub, dmcurve, scal, out=None, status=None):
+        """22 scores per candidate -> ((n, 22) float64, (n,) status)."""
+        bi, dev, keep = self._bates_args(prof, sub, dmcurve, scal, True)
+        n = bi.n
+        if dev:
+            import torch
+
+            if out is None:
+                out = torch.empty((n, 22), dtype=torch.float64, device=prof.device)
+            self._dev(out, "out", (torch.float64,), (n, 22))
+            status = self._status_dev(status, n)
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            out = self._out_host(out, n, 22)
+            status = self._status_host(status, n)
+            flags = 0
         self._check(self.lib.pfe_bates22(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
+        del keep
         return out, status
+
+    def subband3(self, prof, sub, scal, out=None, status=None):
+        """Scores 20-22 alone (pfe_subband3, PHCXOperations.getSubbandParameters):
+        -> ((n, 3) float64, (n,) status)."""
+        bi, dev, keep = self._bates_args(prof, sub, None, scal, False)
+        n = bi.n
+        if dev:
+            import torch
+
+            if out is None:
+                out = torch.empty((n, 3), dtype=torch.float64, device=prof.device)
+            self._dev(out, "out", (torch.float64,), (n, 3))
+            status = self._status_dev(status, n)
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            out = self._out_host(out, n, 3)
+            status = self._status_host(status, n)
+            flags = 0
+        self._check(self.lib.pfe_subband3(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
+        del keep
+        return out, status
+
+    def features30(self, prof, lyon_dm, sub, dmcurve, scal, out=None):
+        """Config 5's feature matrix: the 8 Lyon features (profile + Lyon DM rows) then the
+        22 Bates scores of each candidate -> ((n, 30) float64, (n,) status)."""
+        n = prof.shape[0]
+        dev = _is_device(prof)
+        if dev:
+            import torch
+
+            if out is None:
+                out = torch.empty((n, 30), dtype=torch.float64, device=prof.device)
+            self._dev(out, "out", (torch.float64,), (n, 30))
+            o8 = self.lyon8(prof, lyon_dm)
+            o22, st = self.bates22(prof, sub, dmcurve, scal)
+            out[:, :8].copy_(o8)
+            out[:, 8:].copy_(o22)
+        else:
+            out = self._out_host(out, n, 30)
+            out[:, :8] = self.lyon8(prof, lyon_dm)
+            o22, st = self.bates22(prof, sub, dmcurve, scal)
+            out[:, 8:] = o22
+        return out, st
+
+    # -- PFD -----------------------------------------------------------------------------
+    def _pfd_args(self, profs, subfreqs, scal, fn):
+        if profs.ndim != 4:
+            raise ValueError(f"{fn}: profs must be (n,npart,nsub,L)")
+        n, npart, nsub, L = profs.shape
+        if tuple(subfreqs.shape) != (n, nsub) or tuple(scal.shape) != (n, PFE_PFD_NSCAL):
+            raise ValueError(f"{fn}: subfreqs must be (n,nsub), scal (n,{PFE_PFD_NSCAL})")
+        dev = _is_device(profs)
+        if dev:
+            import torch
+
+            self._dev(profs, "profs", (torch.float64,))
+            self._dev(subfreqs, "subfreqs", (torch.float64,))
+            self._dev(scal, "scal", (torch.float64,))
+            self._follow_torch()
+        else:
+            profs = np.ascontiguousarray(profs, dtype=np.float64)
+            subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
+            scal = np.ascontiguousarray(scal, dtype=np.float64)
+        pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
+        return pin, dev, (profs, subfreqs, scal)
 
     def pfd_dmprof(self, profs, subfreqs, scal, profile=True, chis=True, lyon8=True):
         """PFD preprocessing + Lyon features (pfe_pfd_dmprof) for a batch of folds of one
         shape: profs (n,npart,nsub,L) f64, subfreqs (n,nsub), scal (n,PFE_PFD_NSCAL).
         Returns dict(profile (n,L) f64, chis (n,100) f32, lyon8 (n,8) f64, status (n,))."""
-        n, npart, nsub, L = profs.shape
-        if subfreqs.shape != (n, nsub) or scal.shape != (n, PFE_PFD_NSCAL):
-            raise ValueError("pfd_dmprof: subfreqs must be (n,nsub), scal (n,%d)" % PFE_PFD_NSCAL)
-        dev = _is_device(profs)
+        pin, dev, keep = self._pfd_args(profs, subfreqs, scal, "pfd_dmprof")
+        n, L = pin.n, pin.proflen
         out = {}
         if dev:
             import torch
 
-            self._follow_torch()
             mk = lambda shape, dt: torch.empty(shape, dtype=dt, device=profs.device)  # noqa: E731
             f64, f32, i32 = torch.float64, torch.float32, torch.int32
-            for t in (profs, subfreqs, scal):
-                if not t.is_contiguous():
-                    raise ValueError("pfd_dmprof: device tensors must be contiguous")
             flags = PFE_FLAG_DEVICE_PTRS
         else:
-            profs = np.ascontiguousarray(profs, dtype=np.float64)
-            subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
-            scal = np.ascontiguousarray(scal, dtype=np.float64)
             mk = lambda shape, dt: np.empty(shape, dtype=dt)  # noqa: E731
             f64, f32, i32 = np.float64, np.float32, np.uint32
             flags = 0
@@ -366,44 +569,33 @@ class Engine:
         out["chis"] = mk((n, PFE_PFD_NDM), f32) if chis else None
         out["lyon8"] = mk((n, 8), f64) if lyon8 else None
         out["status"] = mk((n,), i32)
-        pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
         self._check(self.lib.pfe_pfd_dmprof(
             self._h, C.byref(pin), _ptr(out["profile"]) if profile else None,
             _ptr(out["chis"]) if chis else None, _ptr(out["lyon8"]) if lyon8 else None,
             _ptr(out["status"]), flags))
+        del keep
         return out
-
 
     def pfd_bates22(self, profs, subfreqs, scal, out=None, status=None):
         """The 22 scores of PFD folds (pfe_pfd_bates22, PFDFile.compute) for a batch of one
         shape: profs (n,npart,nsub,L) f64, subfreqs (n,nsub), scal (n,PFE_PFD_NSCAL) with
         scal[:, 7] = bary_p1.  Returns (out (n,22) f64, status (n,))."""
-        n, npart, nsub, L = profs.shape
-        if subfreqs.shape != (n, nsub) or scal.shape != (n, PFE_PFD_NSCAL):
-            raise ValueError("pfd_bates22: subfreqs must be (n,nsub), scal (n,%d)" % PFE_PFD_NSCAL)
-        if _is_device(profs):
+        pin, dev, keep = self._pfd_args(profs, subfreqs, scal, "pfd_bates22")
+        n = pin.n
+        if dev:
             import torch
 
-            self._follow_torch()
-            for t in (profs, subfreqs, scal):
-                if not t.is_contiguous():
-                    raise ValueError("pfd_bates22: device tensors must be contiguous")
             if out is None:
                 out = torch.empty((n, 22), dtype=torch.float64, device=profs.device)
-            if status is None:
-                status = torch.empty((n,), dtype=torch.int32, device=profs.device)
+            self._dev(out, "out", (torch.float64,), (n, 22))
+            status = self._status_dev(status, n)
             flags = PFE_FLAG_DEVICE_PTRS
         else:
-            profs = np.ascontiguousarray(profs, dtype=np.float64)
-            subfreqs = np.ascontiguousarray(subfreqs, dtype=np.float64)
-            scal = np.ascontiguousarray(scal, dtype=np.float64)
-            if out is None:
-                out = np.empty((n, 22), dtype=np.float64)
-            if status is None:
-                status = np.empty((n,), dtype=np.uint32)
+            out = self._out_host(out, n, 22)
+            status = self._status_host(status, n)
             flags = 0
-        pin = PfdIn(_ptr(profs), _ptr(subfreqs), _ptr(scal), npart, nsub, L, n)
         self._check(self.lib.pfe_pfd_bates22(self._h, C.byref(pin), _ptr(out), _ptr(status), flags))
+        del keep
         return out, status
 
 

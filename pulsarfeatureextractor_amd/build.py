@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 BUILDDIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIBDIR, "libpfe.so")
-SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip",
+SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip", "subband.hip",
            "pfd.hip", "pfd22.hip"]
 HOST_SOURCES = ["phcx_io.cpp"]  # host-only C++ (PHCX reader / batch packer), built with g++
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]

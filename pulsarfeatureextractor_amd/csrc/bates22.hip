@@ -5,7 +5,6 @@
 //   k_sine (s1-s4) -> k_ghist (+ k_ghist<BIG> for wide histograms) -> k_gt1 (s8,s9)
 //   -> k_gdg (s10,s11) -> k_dmfit (s12-s19) -> k_subband (s20-s22)
 #include <cmath>
-#include <cstdlib>
 
 #include "bates_common.h"
 
@@ -36,10 +35,9 @@ static int blm_fits_per_wave(int64_t n, int cus) {
 
 // Fit slots per wave of the pooled kernels (lm_group.h): a wave works its slots in groups of
 // 4 and runs lmpar one slot per lane, so it wants many; but n / slots waves should still
-// cover the chip's wave slots (CUs x 8) -- PFE_GSLOTS overrides (A/B runs)
-static int glm_slots(int64_t n, int cus) {
-  const char* e = getenv("PFE_GSLOTS");
-  if (e && atoi(e) > 0) return atoi(e) > GLM_FPW ? GLM_FPW : atoi(e);
+// cover the chip's wave slots (CUs x 8) -- the handle option PFE_OPT_GSLOTS overrides
+static int glm_slots(int64_t n, int cus, int fixed) {
+  if (fixed > 0) return fixed > GLM_FPW ? GLM_FPW : fixed;
   const int64_t f = n / ((int64_t)cus * 8);
   return (int)(f < 4 ? 4 : f > GLM_FPW ? GLM_FPW : f);
 }
@@ -66,10 +64,6 @@ static size_t hand_bytes(int64_t n, int region) {
   const int k = region == HAND_GAUSS ? HAND_K_GAUSS : region == HAND_DM ? HAND_K_DM : HAND_K_SINE;
   return (size_t)hand_waves(n, region) * GLM_FPW * k * 16 * sizeof(double);
 }
-static bool hand_on() {
-  const char* e = getenv("PFE_HAND");
-  return !(e && e[0] == '0');
-}
 
 // workspace layout: [GaussWS x n][counters][hand-over regions][per-wave scratch]
 size_t bates22_workspace_bytes(const pfe_bates_in* in) {
@@ -92,13 +86,13 @@ void launch_clear_internal(uint32_t* status, int64_t n, hipStream_t st) {
 
 // workspace pointers, batching parameters and the Freedman-Diaconis constants of a chain
 // over n candidates of lp bins (work: bates22_workspace_bytes)
-void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
+void bates_setup(BatesArgs& a, int64_t n, int lp, void* work, const Options& o) {
   char* wb = (char*)(((uintptr_t)work + 255) & ~(uintptr_t)255);
   a.ws = (GaussWS*)wb;
   wb += align256((size_t)n * sizeof(GaussWS));
   a.counters = (unsigned*)wb;
   wb += align256(BATES_NCOUNTERS * sizeof(unsigned));
-  const bool ho = hand_on();
+  const bool ho = o.handover != 0;
   for (int r = 0; r < 3; ++r) {
     a.hand[r] = ho ? (double*)wb : nullptr;
     wb += align256(hand_bytes(n, r));
@@ -106,7 +100,8 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());
-  a.gslots = glm_slots(n, device_cus());
+  a.gslots = glm_slots(n, device_cus(), o.gslots);
+  a.solver = o.solver;
   a.cus = device_cus();
   a.lp = lp;
   a.n = n;
@@ -116,10 +111,9 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work) {
 }
 
 // fork the three independent score groups onto the handle's side streams (false: serial,
-// when the handle has none or PFE_SERIAL=1)
+// when the handle has none or its PFE_OPT_SERIAL option is set)
 bool fork_begin(const Fork* fk, hipStream_t st) {
-  const char* e = getenv("PFE_SERIAL");
-  if (!fk || !fk->side[0] || (e && e[0] == '1')) return false;
+  if (!fk || !fk->side[0] || fk->serial) return false;
   if (hipEventRecord(fk->ev[0], st) != hipSuccess) return false;
   return hipStreamWaitEvent(fk->side[0], fk->ev[0], 0) == hipSuccess &&
          hipStreamWaitEvent(fk->side[1], fk->ev[0], 0) == hipSuccess;
@@ -133,10 +127,10 @@ hipError_t fork_end(const Fork* fk, hipStream_t st) {
 }
 
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
-                          size_t work_bytes, hipStream_t st, const Fork* fk) {
+                          size_t work_bytes, hipStream_t st, const Fork* fk, const Options& o) {
   if (work_bytes < bates22_workspace_bytes(in)) return hipErrorInvalidValue;
   BatesArgs a;
-  bates_setup(a, in->n, in->lp, work);
+  bates_setup(a, in->n, in->lp, work, o);
   a.prof = in->prof;
   a.fprof = nullptr;
   a.lp = in->lp;

@@ -3,6 +3,7 @@
 
 #include "../../include/pfe.h"
 #include "lm_wave.h"
+#include "options.h"
 
 namespace pfe {
 
@@ -56,6 +57,7 @@ struct BatesArgs {
   int gslots;          // fit slots per wave of the pooled kernels (<= GLM_FPW)
   int cus;             // compute units of the device
   double* hand[3];     // hand-over scratch of the pooled kernels per stream (HAND_*), or null
+  int solver;          // PFE_SOLVER_* (handle option PFE_OPT_SOLVER)
 };
 
 constexpr int BATES_NCOUNTERS = 16;
@@ -71,6 +73,7 @@ constexpr int HAND_K_GAUSS = 24, HAND_K_DM = 24, HAND_K_SINE = 8;
 struct Fork {
   hipStream_t side[2] = {nullptr, nullptr};
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  int serial = 0;  // handle option PFE_OPT_SERIAL: groups in order on the caller's stream
 };
 constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
 constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS state size)

@@ -2024,12 +2024,10 @@ static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }
 
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const int L = a.lp;
-  // batched lmdif (lm_batch.h) unless PFE_BLM=0 selects the wave-per-fit kernels (A/B runs)
-  const char* blm_env = getenv("PFE_BLM");
-  const bool use_blm = !(blm_env && blm_env[0] == '0');
-  // pooled group-LM kernels (lm_group.h) for <= 128 bins unless PFE_GLM=0 (A/B runs)
-  const char* glm_env = getenv("PFE_GLM");
-  const bool use_glm = use_blm && L <= 128 && !(glm_env && glm_env[0] == '0');
+  // batched lmdif (lm_batch.h) unless the handle selects the wave-per-fit kernels
+  const bool use_blm = a.solver != PFE_SOLVER_WAVE;
+  // pooled group-LM kernels (lm_group.h) for <= 128 bins (the default solver)
+  const bool use_glm = a.solver == PFE_SOLVER_POOLED && L <= 128;
   const dim3 pool((unsigned)a.pwaves);
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \

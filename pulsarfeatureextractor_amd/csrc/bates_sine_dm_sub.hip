@@ -1,5 +1,5 @@
-// bates_sine_dm_sub.hip — scores 1-4 (sinusoid fits), 12-19 (candidate parameters and
-// DM-curve fit) and 20-22 (sub-band scores) on gfx950, one wavefront per candidate.
+// bates_sine_dm_sub.hip — scores 1-4 (sinusoid fits) and 12-19 (candidate parameters and
+// DM-curve fit) on gfx950 (scores 20-22: subband.hip).
 //
 // Reference (PulsarFeatureExtractor/src/):
 //   s1-s4   ProfileOperations.getSinusoidFittings :190-376, fitSine :380-491,
@@ -7,8 +7,6 @@
 //   s12-s15 PHCXOperations.getCandidateParameters :81-112; filterScore
 //           CandidateFileInterface.py:84-149;              PHCXFile.py:569-574
 //   s16-s19 PHCXOperations.getDMFittings :121-233;       PHCXFile.py:613-618
-//   s20-s22 PHCXOperations.getSubbandParameters :305-349, getProfileCorr :387-415,
-//           ProfileOperations.getSubband_scores :1585-1686
 #include "bates_common.h"
 #include "lm_batch.h"
 #include "lm_group.h"
@@ -623,442 +621,15 @@ __global__ __launch_bounds__(64, 3) void k_dmfitg(BatesArgs a) {
   glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list, a.hand[HAND_DM], HAND_K_DM);
 }
 
-// ======================================================================================
-// scores 20-22
-// ======================================================================================
-// Pearson correlation as numpy.corrcoef computes it:
-//   c_xy = dot(x-mx, y-my) * (1/(N-1)); r = (c_xy / sqrt(c_xx)) / sqrt(c_yy), clipped to [-1,1]
-__device__ __forceinline__ double corr_from(double cxy, double cxx, double cyy) {
-  double r = (cxy / sqrt(cxx)) / sqrt(cyy);
-  if (r > 1.0) r = 1.0;
-  if (r < -1.0) r = -1.0;
-  return r;  // NaN propagates (clip keeps NaN)
-}
-
-// SL = max sub-band length / 64 slots per lane; NSUB <= 16 sub-bands held in registers.
-template <int SL>
-__global__ __launch_bounds__(BLOCK) void k_subband(BatesArgs a) {
-  constexpr int NSUB = 16;
-  const int64_t c = wave_candidate();
-  if (c >= a.n) return;
-  const int lane = lane_id();
-  const int nsub = a.nsub, lsb = a.lsb;
-  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
-  const int wb = (int)ceil(width * (double)lsb);                     // :1603
-  uint32_t fail = 0;
-  if (wb <= 0 || wb > lsb) fail = PFE_ST_SUBBAND_FAIL;               // m==0 / unbound max_bin
-  if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;                       // corrcoef length mismatch
-  if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
-  if (fail) {
-    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(fail));
-    return;
-  }
-  const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
-  const int nw = lsb - wb + 1;                                       // windows per band
-  // boxcar sums: window j of band i = sum_{b<wb} sub[i][j+b] (integers)
-  double bs[NSUB][SL];
-  double max_bin[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    if (i < nsub) {
-      int best = -1, bestj = 0;
-#pragma unroll
-      for (int k = 0; k < SL; ++k) {
-        const int j = lane + 64 * k;
-        int s = 0;
-        if (j < nw)
-          for (int b = 0; b < wb; ++b) s += sb[i * lsb + j + b];
-        bs[i][k] = (double)s;
-        if (j < nw && s > best) {  // first strict max within the lane (j ascending)
-          best = s;
-          bestj = j;
-        }
-      }
-      // first strict maximum over the wave: largest sum, then lowest index
-      int bv = best, bj = (best >= 0) ? bestj : (1 << 30);
-#pragma unroll
-      for (int s = 1; s < 64; s <<= 1) {
-        const int ov = __shfl_xor(bv, s), oj = __shfl_xor(bj, s);
-        if (ov > bv || (ov == bv && oj < bj)) {
-          bv = ov;
-          bj = oj;
-        }
-      }
-      max_bin[i] = (double)(bj + wb / 2);                            // :1628 (Py2 wb/2)
-    } else {
-      max_bin[i] = 0.0;
-#pragma unroll
-      for (int k = 0; k < SL; ++k) bs[i][k] = 0.0;
-    }
-  }
-  // RMS scatter of the maxima (:1633-1659)
-  double msum = 0.0;
-  for (int i = 0; i < nsub; ++i) msum += max_bin[i];
-  const double med = msum / (double)nsub;
-  int count = 0;
-  double var_med = 0.0;
-  for (int i = 0; i < nsub; ++i)
-    if (fabs(max_bin[i] - med) <= (double)wb) {
-      ++count;
-      var_med += (max_bin[i] - med) * (max_bin[i] - med);
-    }
-  double var;
-  if (count > 1) {
-    var = var_med / (double)(count - 1);
-  } else {
-    double mu = 0.0;
-    for (int i = 0; i < nsub; ++i) mu += max_bin[i];
-    mu /= (double)nsub;
-    var = 0.0;
-    for (int i = 0; i < nsub; ++i) var += (max_bin[i] - mu) * (max_bin[i] - mu);
-    var /= (double)(nsub - 1);
-  }
-  const double rms = sqrt(var) / (double)wb;
-  // centre every band's window sums (numpy.cov subtracts the mean first)
-  const double inv = 1.0 / (double)(nw - 1);
-  {
-    double mean[NSUB];
-#pragma unroll
-    for (int i = 0; i < NSUB; ++i) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < SL; ++k) s += bs[i][k];
-      mean[i] = s;
-    }
-    wsum_arr(mean);
-#pragma unroll
-    for (int i = 0; i < NSUB; ++i) {
-      const double m = mean[i] / (double)nw;
-#pragma unroll
-      for (int k = 0; k < SL; ++k)
-        if (lane + 64 * k < nw) bs[i][k] = bs[i][k] - m;
-        else bs[i][k] = 0.0;
-    }
-  }
-  double var_i[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < SL; ++k) s += bs[i][k] * bs[i][k];
-    var_i[i] = s;
-  }
-  wsum_arr(var_i);
-  // mean pairwise correlation, pairs in the reference's (i<k) order
-  double csum = 0.0;
-  int m = 0;
-#pragma unroll
-  for (int i = 0; i < NSUB - 1; ++i) {
-    if (i + 1 < nsub) {
-      double d[NSUB];
-#pragma unroll
-      for (int k2 = 0; k2 < NSUB; ++k2) {
-        double s = 0.0;
-        if (k2 > i) {
-#pragma unroll
-          for (int k = 0; k < SL; ++k) s += bs[i][k] * bs[k2][k];
-        }
-        d[k2] = s;
-      }
-      wsum_arr(d);
-#pragma unroll
-      for (int k2 = i + 1; k2 < NSUB; ++k2) {
-        if (k2 < nsub) {
-          const double cc = corr_from(d[k2] * inv, var_i[i] * inv, var_i[k2] * inv);
-          if (cc == cc) {
-            csum += cc;
-            ++m;
-          }
-        }
-      }
-    }
-  }
-  if (m == 0) {  // ZeroDivisionError (:1681)
-    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SUBBAND_FAIL));
-    return;
-  }
-  const double mean_corr = csum / (double)m;
-  // s22: sum of |corr(sub_j, profile)| over values > 0.0055 (:403-415, :345-347)
-  double pv[SL];
-  double pm = 0.0;
-#pragma unroll
-  for (int k = 0; k < SL; ++k) {
-    const int j = lane + 64 * k;
-    pv[k] = (j < lsb) ? (double)a.prof[c * a.lp + j] : 0.0;
-    pm += pv[k];
-  }
-  pm = wsum(pm) / (double)lsb;
-  double pvar = 0.0;
-#pragma unroll
-  for (int k = 0; k < SL; ++k) {
-    if (lane + 64 * k < lsb) pv[k] = pv[k] - pm;
-    else pv[k] = 0.0;
-    pvar += pv[k] * pv[k];
-  }
-  pvar = wsum(pvar);
-  const double inv2 = 1.0 / (double)(lsb - 1);
-  double sv[NSUB], dv[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      s += (j < lsb && i < nsub) ? (double)sb[i * lsb + j] : 0.0;
-    }
-    sv[i] = s;
-  }
-  wsum_arr(sv);
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    const double mu = sv[i] / (double)lsb;
-    double d = 0.0, q = 0.0;
-#pragma unroll
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      if (j < lsb && i < nsub) {
-        const double t = (double)sb[i * lsb + j] - mu;
-        d += t * pv[k];
-        q += t * t;
-      }
-    }
-    sv[i] = q;
-    dv[i] = d;
-  }
-  wsum_arr(sv);
-  wsum_arr(dv);
-  double integ = 0.0;
-  for (int i = 0; i < nsub; ++i) {
-    const double cc = fabs(corr_from(dv[i] * inv2, sv[i] * inv2, pvar * inv2));
-    if (cc > 0.0055) integ += cc;
-  }
-  if (lane == 0) {
-    double* o = a.out + c * 22;
-    o[19] = rms;
-    o[20] = mean_corr;
-    o[21] = integ;
-  }
-}
-
-// Sub-bands longer than 128 bins (up to 1024): the integer boxcar sums live in LDS
-// (NSUB x 64*SL ints: 16 KiB at 256 bins, 64 KiB at 1024) and the loops over window slots
-// stay rolled, instead of 16 x SL doubles per lane that spill; same arithmetic, in the same
-// order, as k_subband.
-template <int SL>
-__global__ __launch_bounds__(64) void k_subband_lds(BatesArgs a) {
-  constexpr int NSUB = 16;
-  __shared__ int bsi[NSUB][64 * SL];
-  const int64_t c = blockIdx.x;
-  if (c >= a.n) return;
-  const int lane = lane_id();
-  const int nsub = a.nsub, lsb = a.lsb;
-  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
-  const int wb = (int)ceil(width * (double)lsb);                     // :1603
-  uint32_t fail = 0;
-  if (wb <= 0 || wb > lsb) fail = PFE_ST_SUBBAND_FAIL;
-  if (a.lp != lsb) fail = PFE_ST_SUBBAND_FAIL;
-  if (nsub > NSUB) fail = PFE_ST_UNSUPPORTED;
-  if (fail) {
-    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(fail));
-    return;
-  }
-  const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
-  const int nw = lsb - wb + 1;
-  double max_bin[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) max_bin[i] = 0.0;
-#pragma unroll 1
-  for (int i = 0; i < NSUB; ++i) {
-    int best = -1, bestj = 0;
-#pragma unroll 1
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      int sum = 0;
-      if (i < nsub && j < nw)
-        for (int b = 0; b < wb; ++b) sum += sb[i * lsb + j + b];
-      bsi[i][j] = sum;
-      if (i < nsub && j < nw && sum > best) {
-        best = sum;
-        bestj = j;
-      }
-    }
-    if (i < nsub) {
-      int bv = best, bj = (best >= 0) ? bestj : (1 << 30);
-#pragma unroll
-      for (int st = 1; st < 64; st <<= 1) {
-        const int ov = __shfl_xor(bv, st), oj = __shfl_xor(bj, st);
-        if (ov > bv || (ov == bv && oj < bj)) {
-          bv = ov;
-          bj = oj;
-        }
-      }
-        put(max_bin, i, (double)(bj + wb / 2));
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  double msum = 0.0;
-  for (int i = 0; i < nsub; ++i) msum += max_bin[i];
-  const double med = msum / (double)nsub;
-  int count = 0;
-  double var_med = 0.0;
-  for (int i = 0; i < nsub; ++i)
-    if (fabs(max_bin[i] - med) <= (double)wb) {
-      ++count;
-      var_med += (max_bin[i] - med) * (max_bin[i] - med);
-    }
-  double var;
-  if (count > 1) {
-    var = var_med / (double)(count - 1);
-  } else {
-    double mu = 0.0;
-    for (int i = 0; i < nsub; ++i) mu += max_bin[i];
-    mu /= (double)nsub;
-    var = 0.0;
-    for (int i = 0; i < nsub; ++i) var += (max_bin[i] - mu) * (max_bin[i] - mu);
-    var /= (double)(nsub - 1);
-  }
-  const double rms = sqrt(var) / (double)wb;
-  const double inv = 1.0 / (double)(nw - 1);
-  double bmean[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    double sm = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < SL; ++k) sm += (double)bsi[i][lane + 64 * k];
-    bmean[i] = sm;
-  }
-  wsum_arr(bmean);
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) bmean[i] = bmean[i] / (double)nw;
-  auto cb = [&](int i, int k) -> double {
-    const int j = lane + 64 * k;
-    return (j < nw) ? (double)bsi[i][j] - sel(bmean, i) : 0.0;
-  };
-  double var_i[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    double sm = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      const double v = (j < nw) ? (double)bsi[i][j] - bmean[i] : 0.0;
-      sm += v * v;
-    }
-    var_i[i] = sm;
-  }
-  wsum_arr(var_i);
-  double csum = 0.0;
-  int m = 0;
-#pragma unroll 1
-  for (int i = 0; i + 1 < nsub; ++i) {
-    double d[NSUB];
-#pragma unroll
-    for (int k2 = 0; k2 < NSUB; ++k2) {
-      double sm = 0.0;
-      if (k2 > i) {
-#pragma unroll 1
-        for (int k = 0; k < SL; ++k) {
-          const int j = lane + 64 * k;
-          const double v2 = (j < nw) ? (double)bsi[k2][j] - bmean[k2] : 0.0;
-          sm += cb(i, k) * v2;
-        }
-      }
-      d[k2] = sm;
-    }
-    wsum_arr(d);
-    const double vi = sel(var_i, i);
-#pragma unroll
-    for (int k2 = 0; k2 < NSUB; ++k2) {
-      if (k2 > i && k2 < nsub) {
-        const double cc = corr_from(d[k2] * inv, vi * inv, var_i[k2] * inv);
-        if (cc == cc) {
-          csum += cc;
-          ++m;
-        }
-      }
-    }
-  }
-  if (m == 0) {
-    if (lane == 0) atomicOr(&a.status[c], (uint32_t)(PFE_ST_SUBBAND_FAIL));
-    return;
-  }
-  const double mean_corr = csum / (double)m;
-  double pm = 0.0;
-#pragma unroll 1
-  for (int k = 0; k < SL; ++k) {
-    const int j = lane + 64 * k;
-    pm += (j < lsb) ? (double)a.prof[c * a.lp + j] : 0.0;
-  }
-  pm = wsum(pm) / (double)lsb;
-  auto pvk = [&](int k) -> double {
-    const int j = lane + 64 * k;
-    return (j < lsb) ? (double)a.prof[c * a.lp + j] - pm : 0.0;
-  };
-  double pvar = 0.0;
-#pragma unroll 1
-  for (int k = 0; k < SL; ++k) {
-    const double v = pvk(k);
-    pvar += v * v;
-  }
-  pvar = wsum(pvar);
-  const double inv2 = 1.0 / (double)(lsb - 1);
-  double sv[NSUB], dv[NSUB];
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    double sm = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      sm += (j < lsb && i < nsub) ? (double)sb[i * lsb + j] : 0.0;
-    }
-    sv[i] = sm;
-  }
-  wsum_arr(sv);
-#pragma unroll
-  for (int i = 0; i < NSUB; ++i) {
-    const double mu = sv[i] / (double)lsb;
-    double dd = 0.0, q = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < SL; ++k) {
-      const int j = lane + 64 * k;
-      if (j < lsb && i < nsub) {
-        const double t = (double)sb[i * lsb + j] - mu;
-        dd += t * pvk(k);
-        q += t * t;
-      }
-    }
-    sv[i] = q;
-    dv[i] = dd;
-  }
-  wsum_arr(sv);
-  wsum_arr(dv);
-  double integ = 0.0;
-  for (int i = 0; i < nsub; ++i) {
-    const double cc = fabs(corr_from(dv[i] * inv2, sv[i] * inv2, pvar * inv2));
-    if (cc > 0.0055) integ += cc;
-  }
-  if (lane == 0) {
-    double* o = a.out + c * 22;
-    o[19] = rms;
-    o[20] = mean_corr;
-    o[21] = integ;
-  }
-}
-
 // ---- launchers -----------------------------------------------------------------------
 static inline dim3 grid_waves(int64_t n) { return grid_for_candidates(n); }
 
-// pooled group-LM kernels (lm_group.h) unless PFE_GLM=0 or PFE_BLM=0 (A/B runs)
-static bool glm_on() {
-  const char* g = getenv("PFE_GLM");
-  const char* b = getenv("PFE_BLM");
-  return !(g && g[0] == '0') && !(b && b[0] == '0');
-}
+// pooled group-LM kernels (lm_group.h) unless the handle selects another solver
+static bool glm_on(const BatesArgs& a) { return a.solver == PFE_SOLVER_POOLED; }
 
 template <bool F>
 static void launch_sine_t(const BatesArgs& a, hipStream_t st) {
-  if (glm_on() && a.lp <= 128) {
+  if (glm_on(a) && a.lp <= 128) {
     if (a.lp <= 64)
       hipLaunchKernelGGL((k_sineg<1, F>), pool_grid(a, 3), dim3(64), 0, st, a);
     else
@@ -1084,15 +655,14 @@ hipError_t launch_sine(const BatesArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
-  const char* blm_env = getenv("PFE_BLM");
-  if (glm_on() && a.ndm <= 128) {
+  if (glm_on(a) && a.ndm <= 128) {
     if (a.ndm <= 64)
       hipLaunchKernelGGL(k_dmfitg<1>, pool_grid(a, 3), dim3(64), 0, st, a);
     else
       hipLaunchKernelGGL(k_dmfitg<2>, pool_grid(a, 3), dim3(64), 0, st, a);
     return hipGetLastError();
   }
-  if (!(blm_env && blm_env[0] == '0')) {  // batched lmdif (lm_batch.h)
+  if (a.solver != PFE_SOLVER_WAVE) {  // batched lmdif (lm_batch.h)
     const dim3 g((unsigned)((a.n + a.fpw - 1) / a.fpw));
     if (a.ndm <= 64)
       hipLaunchKernelGGL(k_dmfitb<1>, g, dim3(64), 0, st, a);
@@ -1112,18 +682,6 @@ hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_dmfit<4>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
   else
     hipLaunchKernelGGL(k_dmfit<16>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
-  if (a.lsb <= 64)
-    hipLaunchKernelGGL(k_subband<1>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
-  else if (a.lsb <= 128)
-    hipLaunchKernelGGL(k_subband<2>, grid_waves(a.n), dim3(BLOCK), 0, st, a);
-  else if (a.lsb <= 256)
-    hipLaunchKernelGGL(k_subband_lds<4>, dim3((unsigned)a.n), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(k_subband_lds<16>, dim3((unsigned)a.n), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

@@ -1,11 +1,13 @@
 // capi.hip — extern "C" boundary of libpfe.so (declared in include/pfe.h).
 //
-// Owns: the per-handle HIP stream, device scratch used to stage host buffers, and the
-// argument validation that mirrors the reference's failure behaviour.  No CPU fallback:
-// every compute entry point launches a gfx950 kernel or returns an error.
+// Owns: the per-handle HIP streams, device scratch, the pinned staging ring of the chunked
+// host-pointer path, the handle options and the argument validation that mirrors the
+// reference's failure behaviour.  No CPU fallback: every compute entry point launches a
+// gfx950 kernel or returns an error.
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -14,26 +16,47 @@
 
 #include "../../include/pfe.h"
 #include "bates_common.h"
+#include "options.h"
 #include "pfd.h"
 
 namespace pfe {
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
-                           int64_t ds, int ld, int64_t n, double* out, hipStream_t st);
+                           int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
+                           const Options& o);
 hipError_t launch_lyon8_f64(const double* prof, int64_t ps, int lp, const double* dm,
-                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st);
+                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
+                            const Options& o);
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
-                          size_t work_bytes, hipStream_t st, const Fork* fk);
+                          size_t work_bytes, hipStream_t st, const Fork* fk, const Options& o);
 size_t bates22_workspace_bytes(const pfe_bates_in* in);
+hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, hipStream_t st);
+const char* subband_shape_error(int nsub, int lsb);
 }  // namespace pfe
+
+// chunked host path: device/staging slots in flight (H2D of k+1 | kernel k | D2H of k-1)
+constexpr int PIPE_SLOTS = 3;
+constexpr size_t PIPE_CHUNK_BYTES = 32u << 20;  // input bytes per chunk
 
 struct pfe_handle {
   int device = -1;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   pfe::Fork fork;  // side streams of the 22-score chains (bates_common.h)
-  // staging scratch (device)
+  pfe::Options opt;
+  // device scratch: staging of the one-shot host paths, the 22-score workspace and the
+  // device slots of the chunked host path
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // completion of the last call, on the stream it ran on: a call on another stream first
+  // waits for it, so work on the shared scratch never overlaps
+  hipEvent_t done = nullptr;
+  hipStream_t last = nullptr;
+  bool done_recorded = false;
+  // chunked host path: copy streams, per-slot events and the pinned staging ring
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  hipEvent_t ev_in[PIPE_SLOTS] = {}, ev_k[PIPE_SLOTS] = {}, ev_out[PIPE_SLOTS] = {};
+  void* pin = nullptr;
+  size_t pin_bytes = 0;
   std::string err;
 };
 
@@ -59,9 +82,24 @@ static int set_err(pfe_handle* h, int code, const char* fmt, ...) {
       return set_err((h), PFE_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));     \
   } while (0)
 
+// every compute call: bind the device and order after the previous call of this handle
+static int call_begin(pfe_handle* h) {
+  PFE_HIP(h, hipSetDevice(h->device));
+  if (h->done_recorded && h->last != h->stream) PFE_HIP(h, hipStreamWaitEvent(h->stream, h->done, 0));
+  return PFE_OK;
+}
+static int call_end(pfe_handle* h) {
+  PFE_HIP(h, hipEventRecord(h->done, h->stream));
+  h->done_recorded = true;
+  h->last = h->stream;
+  return PFE_OK;
+}
+
 static int ensure_scratch(pfe_handle* h, size_t bytes) {
   if (bytes <= h->scratch_bytes) return PFE_OK;
   if (h->scratch) {
+    // every earlier call's work on the old scratch has finished before it is freed
+    if (h->done_recorded) PFE_HIP(h, hipEventSynchronize(h->done));
     PFE_HIP(h, hipStreamSynchronize(h->stream));
     PFE_HIP(h, hipFree(h->scratch));
     h->scratch = nullptr;
@@ -73,7 +111,29 @@ static int ensure_scratch(pfe_handle* h, size_t bytes) {
   return PFE_OK;
 }
 
+static int ensure_pinned(pfe_handle* h, size_t bytes) {
+  if (bytes <= h->pin_bytes) return PFE_OK;
+  if (h->pin) {
+    PFE_HIP(h, hipHostFree(h->pin));
+    h->pin = nullptr;
+    h->pin_bytes = 0;
+  }
+  PFE_HIP(h, hipHostMalloc(&h->pin, bytes, hipHostMallocDefault));
+  h->pin_bytes = bytes;
+  return PFE_OK;
+}
+
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// host memory the DMA engines can read directly (hipHostMalloc / hipHostRegister)
+static bool is_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
 
 extern "C" {
 
@@ -113,6 +173,7 @@ int pfe_create(int device, pfe_handle** out) {
     e = hipStreamCreateWithFlags(&h->fork.side[i], hipStreamNonBlocking);
   for (int i = 0; i < 3 && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&h->fork.ev[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     pfe_destroy(h);
     return set_err(nullptr, PFE_EDEVICE, "pfe_create: %s", hipGetErrorString(e));
@@ -124,12 +185,24 @@ int pfe_create(int device, pfe_handle** out) {
 void pfe_destroy(pfe_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  if (h->done_recorded) (void)hipEventSynchronize(h->done);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->h2d) (void)hipStreamSynchronize(h->h2d);
+  if (h->d2h) (void)hipStreamSynchronize(h->d2h);
   if (h->scratch) (void)hipFree(h->scratch);
+  if (h->pin) (void)hipHostFree(h->pin);
   for (hipStream_t& s : h->fork.side)
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t& v : h->fork.ev)
     if (v) (void)hipEventDestroy(v);
+  for (int i = 0; i < PIPE_SLOTS; ++i) {
+    if (h->ev_in[i]) (void)hipEventDestroy(h->ev_in[i]);
+    if (h->ev_k[i]) (void)hipEventDestroy(h->ev_k[i]);
+    if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
+  }
+  if (h->h2d) (void)hipStreamDestroy(h->h2d);
+  if (h->d2h) (void)hipStreamDestroy(h->d2h);
+  if (h->done) (void)hipEventDestroy(h->done);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
@@ -151,7 +224,192 @@ int pfe_synchronize(pfe_handle* h) {
   return PFE_OK;
 }
 
+int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  pfe::Options& o = h->opt;
+  switch (option) {
+    case PFE_OPT_SOLVER:
+      if (v != PFE_SOLVER_POOLED && v != PFE_SOLVER_BATCHED && v != PFE_SOLVER_WAVE) break;
+      o.solver = (int)v;
+      return PFE_OK;
+    case PFE_OPT_SERIAL:
+      if (v != 0 && v != 1) break;
+      o.serial = (int)v;
+      h->fork.serial = (int)v;
+      return PFE_OK;
+    case PFE_OPT_HANDOVER:
+      if (v != 0 && v != 1) break;
+      o.handover = (int)v;
+      return PFE_OK;
+    case PFE_OPT_GSLOTS:
+      if (v < 0 || v > pfe::GLM_FPW) break;
+      o.gslots = (int)v;
+      return PFE_OK;
+    case PFE_OPT_LYON8_BLOCKS:
+      if (v < 1 || v > (1 << 24)) break;
+      o.lyon8_blocks = (int)v;
+      return PFE_OK;
+    case PFE_OPT_LYON8_BURST:
+      if (v != 1 && v != 2 && v != 4) break;
+      o.lyon8_burst = (int)v;
+      return PFE_OK;
+    case PFE_OPT_PFD_WAVES:
+      if (v != 1 && v != 4) break;
+      o.pfd_waves = (int)v;
+      return PFE_OK;
+    default:
+      return set_err(h, PFE_EINVAL, "pfe_set_option: unknown option %d", option);
+  }
+  return set_err(h, PFE_EINVAL, "pfe_set_option: value %lld out of range for option %d",
+                 (long long)v, option);
+}
+
+int pfe_get_option(const pfe_handle* h, int32_t option, int64_t* v) {
+  if (!h || !v) return PFE_EINVAL;
+  const pfe::Options& o = h->opt;
+  switch (option) {
+    case PFE_OPT_SOLVER: *v = o.solver; return PFE_OK;
+    case PFE_OPT_SERIAL: *v = o.serial; return PFE_OK;
+    case PFE_OPT_HANDOVER: *v = o.handover; return PFE_OK;
+    case PFE_OPT_GSLOTS: *v = o.gslots; return PFE_OK;
+    case PFE_OPT_LYON8_BLOCKS: *v = o.lyon8_blocks; return PFE_OK;
+    case PFE_OPT_LYON8_BURST: *v = o.lyon8_burst; return PFE_OK;
+    case PFE_OPT_PFD_WAVES: *v = o.pfd_waves; return PFE_OK;
+    default: return PFE_EINVAL;
+  }
+}
+
+int pfe_host_alloc(size_t bytes, void** out) {
+  if (!out) return PFE_EINVAL;
+  *out = nullptr;
+  if (bytes == 0) bytes = 1;
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return PFE_EDEVICE;
+  }
+  return PFE_OK;
+}
+
+void pfe_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 }  // extern "C"
+
+// ---- 8 Lyon features ------------------------------------------------------------------
+template <typename T>
+static hipError_t launch_lyon8(const T* prof, int64_t ps, int lp, const T* dm, int64_t ds, int ld,
+                               int64_t n, double* out, hipStream_t st, const pfe::Options& o) {
+  if constexpr (sizeof(T) == 1)
+    return pfe::launch_lyon8_u8((const uint8_t*)prof, ps, lp, (const uint8_t*)dm, ds, ld, n, out,
+                                st, o);
+  else
+    return pfe::launch_lyon8_f64((const double*)prof, ps, lp, (const double*)dm, ds, ld, n, out,
+                                 st, o);
+}
+
+// rows [r0, r0 + rows) of a strided host array into a dense buffer
+template <typename T>
+static void pack_rows(T* dst, const T* src, int64_t stride, int len, int64_t r0, int64_t rows) {
+  if (stride == len) {
+    memcpy(dst, src + r0 * stride, (size_t)rows * len * sizeof(T));
+    return;
+  }
+  for (int64_t r = 0; r < rows; ++r)
+    memcpy(dst + r * len, src + (r0 + r) * stride, (size_t)len * sizeof(T));
+}
+
+// The host-pointer path, chunked and pipelined: chunk k's rows go host -> HBM on the h2d
+// stream while chunk k-1's kernel runs on the handle's stream and chunk k-2's features go
+// back on the d2h stream.  Pinned caller buffers (pfe_host_alloc) are DMA'd in place;
+// pageable ones are packed into (or unpacked from) the handle's pinned staging ring by the
+// calling thread, overlapped with the DMA of the other slots.
+template <typename T>
+static int lyon8_host(pfe_handle* h, const T* prof, int64_t ps, int32_t lp, const T* dm,
+                      int64_t ds, int32_t ld, int64_t n, double* out) {
+  const size_t row_in = (size_t)(lp + ld) * sizeof(T);
+  int64_t chunk = (int64_t)(PIPE_CHUNK_BYTES / row_in);
+  chunk = std::max<int64_t>(1024, chunk & ~(int64_t)63);
+  if (chunk > n) chunk = n;
+  const size_t pb = align256((size_t)chunk * lp * sizeof(T));
+  const size_t db = align256((size_t)chunk * ld * sizeof(T));
+  const size_t ob = align256((size_t)chunk * 8 * sizeof(double));
+  const size_t slot = pb + db + ob;
+  int rc = ensure_scratch(h, PIPE_SLOTS * slot);
+  if (rc) return rc;
+  const bool pin_p = is_pinned(prof), pin_d = is_pinned(dm), pin_o = is_pinned(out);
+  if (!(pin_p && pin_d && pin_o)) {
+    rc = ensure_pinned(h, PIPE_SLOTS * slot);
+    if (rc) return rc;
+  }
+  if (!h->h2d) {
+    PFE_HIP(h, hipStreamCreateWithFlags(&h->h2d, hipStreamNonBlocking));
+    PFE_HIP(h, hipStreamCreateWithFlags(&h->d2h, hipStreamNonBlocking));
+    for (int i = 0; i < PIPE_SLOTS; ++i) {
+      PFE_HIP(h, hipEventCreateWithFlags(&h->ev_in[i], hipEventDisableTiming));
+      PFE_HIP(h, hipEventCreateWithFlags(&h->ev_k[i], hipEventDisableTiming));
+      PFE_HIP(h, hipEventCreateWithFlags(&h->ev_out[i], hipEventDisableTiming));
+    }
+  }
+  // the copy streams start after the work already queued on the handle's stream
+  PFE_HIP(h, hipEventRecord(h->done, h->stream));
+  PFE_HIP(h, hipStreamWaitEvent(h->h2d, h->done, 0));
+  PFE_HIP(h, hipStreamWaitEvent(h->d2h, h->done, 0));
+  const int64_t K = (n + chunk - 1) / chunk;
+  auto rows_of = [&](int64_t k) { return std::min<int64_t>(chunk, n - k * chunk); };
+  auto unstage_out = [&](int64_t k) -> int {  // pageable out: staging -> caller, after D2H k
+    const int s = (int)(k % PIPE_SLOTS);
+    PFE_HIP(h, hipEventSynchronize(h->ev_out[s]));
+    if (!pin_o)
+      memcpy(out + k * chunk * 8, (char*)h->pin + s * slot + pb + db,
+             (size_t)rows_of(k) * 8 * sizeof(double));
+    return PFE_OK;
+  };
+  for (int64_t k = 0; k < K; ++k) {
+    const int s = (int)(k % PIPE_SLOTS);
+    const int64_t r0 = k * chunk, rows = rows_of(k);
+    char* dslot = (char*)h->scratch + s * slot;
+    char* hslot = h->pin ? (char*)h->pin + s * slot : nullptr;
+    T* dprof = (T*)dslot;
+    T* ddm = (T*)(dslot + pb);
+    double* dout = (double*)(dslot + pb + db);
+    if (k >= PIPE_SLOTS) {
+      // slot reuse: chunk k-3's staged output is drained (and with it its H2D and kernel)
+      rc = unstage_out(k - PIPE_SLOTS);
+      if (rc) return rc;
+    }
+    if (!pin_p) pack_rows((T*)hslot, prof, ps, lp, r0, rows);
+    if (!pin_d) pack_rows((T*)(hslot + pb), dm, ds, ld, r0, rows);
+    if (pin_p)
+      PFE_HIP(h, hipMemcpy2DAsync(dprof, lp * sizeof(T), prof + r0 * ps, ps * sizeof(T),
+                                  lp * sizeof(T), rows, hipMemcpyHostToDevice, h->h2d));
+    else
+      PFE_HIP(h, hipMemcpyAsync(dprof, hslot, (size_t)rows * lp * sizeof(T),
+                                hipMemcpyHostToDevice, h->h2d));
+    if (pin_d)
+      PFE_HIP(h, hipMemcpy2DAsync(ddm, ld * sizeof(T), dm + r0 * ds, ds * sizeof(T),
+                                  ld * sizeof(T), rows, hipMemcpyHostToDevice, h->h2d));
+    else
+      PFE_HIP(h, hipMemcpyAsync(ddm, hslot + pb, (size_t)rows * ld * sizeof(T),
+                                hipMemcpyHostToDevice, h->h2d));
+    PFE_HIP(h, hipEventRecord(h->ev_in[s], h->h2d));
+    PFE_HIP(h, hipStreamWaitEvent(h->stream, h->ev_in[s], 0));
+    hipError_t e = launch_lyon8<T>(dprof, lp, lp, ddm, ld, ld, rows, dout, h->stream, h->opt);
+    if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "lyon8 launch: %s", hipGetErrorString(e));
+    PFE_HIP(h, hipEventRecord(h->ev_k[s], h->stream));
+    PFE_HIP(h, hipStreamWaitEvent(h->d2h, h->ev_k[s], 0));
+    PFE_HIP(h, hipMemcpyAsync(pin_o ? (void*)(out + r0 * 8) : (void*)(hslot + pb + db), dout,
+                              (size_t)rows * 8 * sizeof(double), hipMemcpyDeviceToHost, h->d2h));
+    PFE_HIP(h, hipEventRecord(h->ev_out[s], h->d2h));
+  }
+  for (int64_t k = std::max<int64_t>(0, K - PIPE_SLOTS); k < K; ++k) {
+    rc = unstage_out(k);
+    if (rc) return rc;
+  }
+  return PFE_OK;
+}
 
 template <typename T>
 static int lyon8_impl(pfe_handle* h, const T* prof, int64_t ps, int32_t lp, const T* dm,
@@ -170,48 +428,18 @@ static int lyon8_impl(pfe_handle* h, const T* prof, int64_t ps, int32_t lp, cons
     return set_err(h, PFE_EINVAL, "lyon8: row too long");
   if (is_u8 && (lp >= (1 << 24) || ld >= (1 << 24)))
     return set_err(h, PFE_EINVAL, "lyon8_u8: rows must be shorter than 2^24 bins");
-  PFE_HIP(h, hipSetDevice(h->device));
-  hipStream_t st = h->stream;
-  const T* dprof = prof;
-  const T* ddm = dm;
-  double* dout = out;
-  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
-    // stage dense copies of the rows (row strides collapse to lengths)
-    const size_t pb = align256((size_t)n * lp * sizeof(T));
-    const size_t db = align256((size_t)n * ld * sizeof(T));
-    const size_t ob = align256((size_t)n * 8 * sizeof(double));
-    int rc = ensure_scratch(h, pb + db + ob);
-    if (rc) return rc;
-    char* base = (char*)h->scratch;
-    PFE_HIP(h, hipMemcpy2DAsync(base, lp * sizeof(T), prof, ps * sizeof(T), lp * sizeof(T), n,
-                                hipMemcpyHostToDevice, st));
-    PFE_HIP(h, hipMemcpy2DAsync(base + pb, ld * sizeof(T), dm, ds * sizeof(T), ld * sizeof(T), n,
-                                hipMemcpyHostToDevice, st));
-    dprof = (const T*)base;
-    ddm = (const T*)(base + pb);
-    dout = (double*)(base + pb + db);
-    ps = lp;
-    ds = ld;
+  int rc = call_begin(h);
+  if (rc) return rc;
+  if (flags & PFE_FLAG_DEVICE_PTRS) {
+    hipError_t e = launch_lyon8<T>(prof, ps, lp, dm, ds, ld, n, out, h->stream, h->opt);
+    if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "lyon8 launch: %s", hipGetErrorString(e));
+    if (status) PFE_HIP(h, hipMemsetAsync(status, 0, (size_t)n * sizeof(uint32_t), h->stream));
+    return call_end(h);
   }
-  hipError_t e;
-  if constexpr (sizeof(T) == 1)
-    e = pfe::launch_lyon8_u8((const uint8_t*)dprof, ps, lp, (const uint8_t*)ddm, ds, ld, n,
-                             dout, st);
-  else
-    e = pfe::launch_lyon8_f64((const double*)dprof, ps, lp, (const double*)ddm, ds, ld, n,
-                              dout, st);
-  if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "lyon8 launch: %s", hipGetErrorString(e));
-  if (status) {
-    if (flags & PFE_FLAG_DEVICE_PTRS)
-      PFE_HIP(h, hipMemsetAsync(status, 0, (size_t)n * sizeof(uint32_t), st));
-    else
-      memset(status, 0, (size_t)n * sizeof(uint32_t));
-  }
-  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
-    PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 8 * sizeof(double), hipMemcpyDeviceToHost, st));
-    PFE_HIP(h, hipStreamSynchronize(st));
-  }
-  return PFE_OK;
+  rc = lyon8_host<T>(h, prof, ps, lp, dm, ds, ld, n, out);
+  if (rc) return rc;
+  if (status) memset(status, 0, (size_t)n * sizeof(uint32_t));
+  return call_end(h);
 }
 
 extern "C" {
@@ -228,6 +456,62 @@ int pfe_lyon8_f64(pfe_handle* h, const double* prof, int64_t ps, int32_t lp, con
   return lyon8_impl<double>(h, prof, ps, lp, dm, ds, ld, n, out, status, flags, false);
 }
 
+}  // extern "C"
+
+// ---- 22 Bates scores / sub-band scores -------------------------------------------------
+static int check_bates_in(pfe_handle* h, const pfe_bates_in* in, const char* fn, bool need_dm) {
+  if (!in->prof || !in->sub || !in->scal || (need_dm && !in->dmcurve))
+    return set_err(h, PFE_EINVAL, "%s: null input array", fn);
+  if (in->lp < 8 || in->lp > 1024)
+    return set_err(h, PFE_EINVAL, "%s: lp=%d outside [8,1024]", fn, in->lp);
+  if (const char* why = pfe::subband_shape_error(in->nsub, in->lsb))
+    return set_err(h, PFE_EINVAL, "%s: sub-band shape %dx%d: %s", fn, in->nsub, in->lsb, why);
+  if (need_dm && (in->ndm < 3 || in->ndm > 1024))
+    return set_err(h, PFE_EINVAL, "%s: ndm=%d outside [3,1024]", fn, in->ndm);
+  return PFE_OK;
+}
+
+// one-shot staging of a host-pointer batch: inputs -> scratch, then `nout` doubles and a
+// status word per row of output space
+static int stage_bates(pfe_handle* h, const pfe_bates_in* in, pfe_bates_in& din, int nout,
+                       bool with_dm, size_t work, double*& dout, uint32_t*& dstat, size_t& off) {
+  const int64_t n = in->n;
+  hipStream_t st = h->stream;
+  const size_t pb = align256((size_t)n * in->lp);
+  const size_t sb = align256((size_t)n * in->nsub * in->lsb);
+  const size_t db = with_dm ? align256((size_t)n * in->ndm * sizeof(double)) : 0;
+  const size_t cb = align256((size_t)n * PFE_NSCAL * sizeof(double));
+  const size_t ob = align256((size_t)n * nout * sizeof(double));
+  const size_t tb = align256((size_t)n * sizeof(uint32_t));
+  int rc = ensure_scratch(h, pb + sb + db + cb + ob + tb + work);
+  if (rc) return rc;
+  char* base = (char*)h->scratch;
+  PFE_HIP(h, hipMemcpyAsync(base, in->prof, (size_t)n * in->lp, hipMemcpyHostToDevice, st));
+  din.prof = (const uint8_t*)base;
+  off = pb;
+  PFE_HIP(h, hipMemcpyAsync(base + off, in->sub, (size_t)n * in->nsub * in->lsb,
+                            hipMemcpyHostToDevice, st));
+  din.sub = (const uint8_t*)(base + off);
+  off += sb;
+  if (with_dm) {
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->dmcurve, (size_t)n * in->ndm * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    din.dmcurve = (const double*)(base + off);
+    off += db;
+  }
+  PFE_HIP(h, hipMemcpyAsync(base + off, in->scal, (size_t)n * PFE_NSCAL * sizeof(double),
+                            hipMemcpyHostToDevice, st));
+  din.scal = (const double*)(base + off);
+  off += cb;
+  dout = (double*)(base + off);
+  off += ob;
+  dstat = (uint32_t*)(base + off);
+  off += tb;
+  return PFE_OK;
+}
+
+extern "C" {
+
 int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
                 uint32_t flags) {
   if (!h) return PFE_EINVAL;
@@ -236,15 +520,10 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
   const int64_t n = in->n;
   if (n < 0) return set_err(h, PFE_EINVAL, "bates22: n < 0");
   if (n == 0) return PFE_OK;
-  if (!in->prof || !in->sub || !in->dmcurve || !in->scal)
-    return set_err(h, PFE_EINVAL, "bates22: null input array");
-  if (in->lp < 8 || in->lp > 1024)
-    return set_err(h, PFE_EINVAL, "bates22: lp=%d outside [8,1024]", in->lp);
-  if (in->nsub < 2 || in->nsub > 64 || in->lsb < 1 || in->lsb > 1024)
-    return set_err(h, PFE_EINVAL, "bates22: sub-band shape %dx%d unsupported", in->nsub, in->lsb);
-  if (in->ndm < 3 || in->ndm > 1024)
-    return set_err(h, PFE_EINVAL, "bates22: ndm=%d outside [3,1024]", in->ndm);
-  PFE_HIP(h, hipSetDevice(h->device));
+  int rc = check_bates_in(h, in, "bates22", true);
+  if (rc) return rc;
+  rc = call_begin(h);
+  if (rc) return rc;
   hipStream_t st = h->stream;
   pfe_bates_in din = *in;
   double* dout = out;
@@ -252,48 +531,54 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
   size_t off = 0;
   const size_t work = pfe::bates22_workspace_bytes(in);
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
-    const size_t pb = align256((size_t)n * in->lp);
-    const size_t sb = align256((size_t)n * in->nsub * in->lsb);
-    const size_t db = align256((size_t)n * in->ndm * sizeof(double));
-    const size_t cb = align256((size_t)n * PFE_NSCAL * sizeof(double));
-    const size_t ob = align256((size_t)n * 22 * sizeof(double));
-    const size_t tb = align256((size_t)n * sizeof(uint32_t));
-    int rc = ensure_scratch(h, pb + sb + db + cb + ob + tb + work);
-    if (rc) return rc;
-    char* base = (char*)h->scratch;
-    PFE_HIP(h, hipMemcpyAsync(base, in->prof, (size_t)n * in->lp, hipMemcpyHostToDevice, st));
-    din.prof = (const uint8_t*)base;
-    off = pb;
-    PFE_HIP(h, hipMemcpyAsync(base + off, in->sub, (size_t)n * in->nsub * in->lsb,
-                              hipMemcpyHostToDevice, st));
-    din.sub = (const uint8_t*)(base + off);
-    off += sb;
-    PFE_HIP(h, hipMemcpyAsync(base + off, in->dmcurve, (size_t)n * in->ndm * sizeof(double),
-                              hipMemcpyHostToDevice, st));
-    din.dmcurve = (const double*)(base + off);
-    off += db;
-    PFE_HIP(h, hipMemcpyAsync(base + off, in->scal, (size_t)n * PFE_NSCAL * sizeof(double),
-                              hipMemcpyHostToDevice, st));
-    din.scal = (const double*)(base + off);
-    off += cb;
-    dout = (double*)(base + off);
-    off += ob;
-    dstat = (uint32_t*)(base + off);
-    off += tb;
+    rc = stage_bates(h, in, din, 22, true, work, dout, dstat, off);
   } else {
-    int rc = ensure_scratch(h, work);
-    if (rc) return rc;
+    rc = ensure_scratch(h, work);
   }
-  hipError_t e = pfe::launch_bates22(&din, dout, dstat, (char*)h->scratch + off, work, st, &h->fork);
+  if (rc) return rc;
+  hipError_t e = pfe::launch_bates22(&din, dout, dstat, (char*)h->scratch + off, work, st,
+                                     &h->fork, h->opt);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "bates22 launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipStreamSynchronize(st));
   }
-  return PFE_OK;
+  return call_end(h);
 }
 
+int pfe_subband3(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                 uint32_t flags) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  if (!in || !out || !status) return set_err(h, PFE_EINVAL, "subband3: null argument");
+  const int64_t n = in->n;
+  if (n < 0) return set_err(h, PFE_EINVAL, "subband3: n < 0");
+  if (n == 0) return PFE_OK;
+  int rc = check_bates_in(h, in, "subband3", false);
+  if (rc) return rc;
+  rc = call_begin(h);
+  if (rc) return rc;
+  hipStream_t st = h->stream;
+  pfe_bates_in din = *in;
+  double* dout = out;
+  uint32_t* dstat = status;
+  size_t off = 0;
+  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
+    rc = stage_bates(h, in, din, 3, false, 0, dout, dstat, off);
+    if (rc) return rc;
+  }
+  hipError_t e = pfe::launch_subband3(&din, dout, dstat, st);
+  if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "subband3 launch: %s", hipGetErrorString(e));
+  if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
+    PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipStreamSynchronize(st));
+  }
+  return call_end(h);
+}
+
+// ---- PFD -------------------------------------------------------------------------------
 int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* chis,
                    double* lyon8, uint32_t* status, uint32_t flags) {
   if (!h) return PFE_EINVAL;
@@ -309,13 +594,15 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
   if (pfe::pfd_lds_bytes(in->nsub, in->proflen) > 160 * 1024)
     return set_err(h, PFE_EINVAL, "pfd_dmprof: nsub*proflen=%d exceeds the LDS-resident limit",
                    in->nsub * in->proflen);
-  PFE_HIP(h, hipSetDevice(h->device));
+  int rc = call_begin(h);
+  if (rc) return rc;
   hipStream_t st = h->stream;
   pfe::PfdArgs a;
   a.npart = in->npart;
   a.nsub = in->nsub;
   a.L = in->proflen;
   a.n = n;
+  a.waves = h->opt.pfd_waves;
   const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
   if (flags & PFE_FLAG_DEVICE_PTRS) {
     a.profs = in->profs;
@@ -333,7 +620,7 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
     const size_t xb = chis ? align256((size_t)n * PFE_PFD_NDM * sizeof(float)) : 0;
     const size_t lb = lyon8 ? align256((size_t)n * 8 * sizeof(double)) : 0;
     const size_t tb = align256((size_t)n * sizeof(uint32_t));
-    int rc = ensure_scratch(h, pb + fb + cb + ob + xb + lb + tb);
+    rc = ensure_scratch(h, pb + fb + cb + ob + xb + lb + tb);
     if (rc) return rc;
     char* base = (char*)h->scratch;
     size_t off = 0;
@@ -372,7 +659,7 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
                               hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipStreamSynchronize(st));
   }
-  return PFE_OK;
+  return call_end(h);
 }
 
 int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* status,
@@ -391,20 +678,22 @@ int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* 
   if (pfe::pfd_lds_bytes(in->nsub, in->proflen) > 160 * 1024)
     return set_err(h, PFE_EINVAL, "pfd_bates22: nsub*proflen=%d exceeds the LDS-resident limit",
                    in->nsub * in->proflen);
-  PFE_HIP(h, hipSetDevice(h->device));
+  int rc = call_begin(h);
+  if (rc) return rc;
   hipStream_t st = h->stream;
   pfe::PfdArgs a;
   a.npart = in->npart;
   a.nsub = in->nsub;
   a.L = in->proflen;
   a.n = n;
+  a.waves = h->opt.pfd_waves;
   const size_t work = pfe::pfd22_workspace_bytes(n, in->proflen);
   const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
   double* dout = out;
   uint32_t* dstat = status;
   size_t off = 0;
   if (flags & PFE_FLAG_DEVICE_PTRS) {
-    int rc = ensure_scratch(h, work);
+    rc = ensure_scratch(h, work);
     if (rc) return rc;
     a.profs = in->profs;
     a.subfreqs = in->subfreqs;
@@ -415,7 +704,7 @@ int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* 
     const size_t cb = align256((size_t)n * PFE_PFD_NSCAL * sizeof(double));
     const size_t ob = align256((size_t)n * 22 * sizeof(double));
     const size_t tb = align256((size_t)n * sizeof(uint32_t));
-    int rc = ensure_scratch(h, pb + fb + cb + ob + tb + work);
+    rc = ensure_scratch(h, pb + fb + cb + ob + tb + work);
     if (rc) return rc;
     char* base = (char*)h->scratch;
     PFE_HIP(h, hipMemcpyAsync(base, in->profs, np * sizeof(double), hipMemcpyHostToDevice, st));
@@ -434,14 +723,15 @@ int pfe_pfd_bates22(pfe_handle* h, const pfe_pfd_in* in, double* out, uint32_t* 
     dstat = (uint32_t*)(base + off);
     off += tb;
   }
-  hipError_t e = pfe::launch_pfd22(a, dout, dstat, (char*)h->scratch + off, work, st, &h->fork);
+  hipError_t e = pfe::launch_pfd22(a, dout, dstat, (char*)h->scratch + off, work, st, &h->fork,
+                                   h->opt);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "pfd_bates22 launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 22 * sizeof(double), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipStreamSynchronize(st));
   }
-  return PFE_OK;
+  return call_end(h);
 }
 
 }  // extern "C"

@@ -9,10 +9,9 @@
 // (DataProcessor.py:884-886).
 //
 // Design (HBM-bound streaming reduction, no MFMA):
-//   * PHCX bins are 02X bytes, so all power sums are EXACT integers.  We form
-//     y = x - 128 (a byte XOR), and accumulate T1..T4 = sum y^k with the gfx950 packed
-//     integer dot instructions (v_dot4_i32_i8 for y and y^2, v_dot2_{i32_i16,u32_u16} for
-//     y^3 and y^4 on packed 16-bit squares).  ~3.3 VALU ops per input byte.
+//   * PHCX bins are 02X bytes, so all power sums are EXACT integers: sum x and sum x^2 with
+//     v_dot4_u32_u8, and with y = x - 128 unpacked to 16-bit halves, sum y^3 and sum y^4
+//     with v_dot2_{i32_i16,u32_u16} on packed 16-bit squares.  ~3.3 VALU ops per byte.
 //   * The exact central-moment numerators n^k*m_k come from T1..T4 in 64-bit modular
 //     integer arithmetic (exact for n <= 430; a 128-bit variant covers long DM arrays),
 //     so each m_k is correctly rounded from its exact rational value: mean and std match
@@ -26,8 +25,7 @@
 //   * Generic path (any lengths/alignment): one wave per (candidate,row), byte loads,
 //     64-bit per-lane sums, 128-bit finalisation.
 
-#include <cstdlib>
-
+#include "options.h"
 #include "pfe_common.h"
 
 namespace pfe {
@@ -36,41 +34,6 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
-
-struct RowSums {
-  int t1;        // sum y        (|.| <= 128*L)
-  int t2;        // sum y^2      (<= 16384*L)
-  int t3;        // sum y^3      (|.| <= 2^21*L)
-  uint64_t t4;   // sum y^4      (<= 2^28*L)
-};
-
-// Accumulate 4 bytes packed in x into the row sums.  t4a is a 32-bit partial for y^4
-// (<= 2^29 added per call); callers flush it to 64 bits every 2 calls.
-__device__ __forceinline__ void acc_dword(uint32_t x, int& t1, int& t2, int& t3, uint32_t& t4a) {
-  const uint32_t v = x ^ 0x80808080u;  // bytes are now two's-complement y = x-128
-  t1 = __builtin_amdgcn_sdot4((int)v, 0x01010101, t1, false);
-  t2 = __builtin_amdgcn_sdot4((int)v, (int)v, t2, false);
-  // zero-extend bytes {0,2} and {1,3} into 16-bit halves
-  const uint32_t lo = x & 0x00FF00FFu;
-  const uint32_t hi = (x >> 8) & 0x00FF00FFu;
-  short2v ylo = __builtin_bit_cast(short2v, lo) - (short2v){128, 128};
-  short2v yhi = __builtin_bit_cast(short2v, hi) - (short2v){128, 128};
-  ushort2v qlo = __builtin_bit_cast(ushort2v, ylo) * __builtin_bit_cast(ushort2v, ylo);  // y^2 <= 16384
-  ushort2v qhi = __builtin_bit_cast(ushort2v, yhi) * __builtin_bit_cast(ushort2v, yhi);
-  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qlo), ylo, t3, false);
-  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qhi), yhi, t3, false);
-  t4a = __builtin_amdgcn_udot2(qlo, qlo, t4a, false);
-  t4a = __builtin_amdgcn_udot2(qhi, qhi, t4a, false);
-}
-
-__device__ __forceinline__ void acc_uint4(const u32x4 q, RowSums& s) {
-  uint32_t a = 0, b = 0;
-  acc_dword(q.x, s.t1, s.t2, s.t3, a);
-  acc_dword(q.y, s.t1, s.t2, s.t3, a);
-  acc_dword(q.z, s.t1, s.t2, s.t3, b);
-  acc_dword(q.w, s.t1, s.t2, s.t3, b);
-  s.t4 += (uint64_t)a + (uint64_t)b;
-}
 
 // Exact central-moment numerators from shifted power sums (y = x - 128):
 //   N2 = n^2 m2 = n T2 - T1^2
@@ -143,77 +106,11 @@ __device__ __forceinline__ double stat_k(const Moments& m, int k) {
   return m.m4 / (m.m2 * m.m2) - 3.0;
 }
 
-// ---- fast path -------------------------------------------------------------------------
-// L in {64,128,256}; LPC = L/32 lanes per candidate; each lane: 32 B of each row.
-template <int L>
-__global__ __launch_bounds__(256) void lyon8_u8_fast(const uint8_t* __restrict__ prof,
-                                                     int64_t ps,
-                                                     const uint8_t* __restrict__ dm,
-                                                     int64_t ds, int64_t n,
-                                                     double* __restrict__ out) {
-  constexpr int LPC = L / 32;       // lanes per candidate: 2, 4, 8
-  constexpr int CPW = 64 / LPC;     // candidates per wave step
-  constexpr int SPL = 8 / LPC;      // outputs per lane: 4, 2, 1
-  const int lane = threadIdx.x & 63;
-  const int sub = lane % LPC;
-  const int cw = lane / LPC;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-
-  for (int64_t base = wave * CPW; base < n; base += nwaves * CPW) {
-    const int64_t c = base + cw;
-    const bool valid = c < n;
-    u32x4 p0 = {0, 0, 0, 0}, p1 = p0, d0 = p0, d1 = p0;
-    if (valid) {
-      const u32x4* pp = reinterpret_cast<const u32x4*>(prof + c * ps + sub * 32);
-      const u32x4* dp = reinterpret_cast<const u32x4*>(dm + c * ds + sub * 32);
-      p0 = __builtin_nontemporal_load(pp);
-      p1 = __builtin_nontemporal_load(pp + 1);
-      d0 = __builtin_nontemporal_load(dp);
-      d1 = __builtin_nontemporal_load(dp + 1);
-    }
-    RowSums sp = {0, 0, 0, 0}, sd = {0, 0, 0, 0};
-    acc_uint4(p0, sp);
-    acc_uint4(p1, sp);
-    acc_uint4(d0, sd);
-    acc_uint4(d1, sd);
-    sp.t1 = group_sum_i32<LPC>(sp.t1);
-    sp.t2 = group_sum_i32<LPC>(sp.t2);
-    sp.t3 = group_sum_i32<LPC>(sp.t3);
-    sp.t4 = group_sum_u64<LPC>(sp.t4);
-    sd.t1 = group_sum_i32<LPC>(sd.t1);
-    sd.t2 = group_sum_i32<LPC>(sd.t2);
-    sd.t3 = group_sum_i32<LPC>(sd.t3);
-    sd.t4 = group_sum_u64<LPC>(sd.t4);
-    // this lane's outputs: j0 .. j0+SPL-1 of the candidate's 8 (profile 0-3, DM 4-7)
-    const int j0 = sub * SPL;
-    const bool is_dm = j0 >= 4;
-    const RowSums& s = is_dm ? sd : sp;
-    const Moments m = moments_i64(L, s.t1, s.t2, s.t3, s.t4);
-    if (valid) {
-      double* o = out + c * 8 + j0;
-      if constexpr (SPL == 4) {
-        f64x2 a = {stat_k(m, 0), stat_k(m, 1)};
-        f64x2 b = {stat_k(m, 2), stat_k(m, 3)};
-        __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(o));
-        __builtin_nontemporal_store(b, reinterpret_cast<f64x2*>(o) + 1);
-      } else if constexpr (SPL == 2) {
-        const int k0 = j0 & 3;
-        f64x2 a = {stat_k(m, k0), stat_k(m, k0 + 1)};
-        __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(o));
-      } else {
-        __builtin_nontemporal_store(stat_k(m, j0 & 3), o);
-      }
-    }
-  }
-}
-
-// ---- fast path, v2 -------------------------------------------------------------------
-// Same lane mapping as lyon8_u8_fast; per 4 bytes: S1 = sum x and S2 = sum x^2 by unsigned
-// v_dot4 (no XOR), the shifted y = x-128 only for y^3/y^4 (v_perm unpack, packed i16
-// sub/mul, v_dot2); branch-free finalisation with compile-time powers of 1/L (exact for
-// L = 2^k, so mean and m2..m4 are the correctly rounded rationals with no division); the
-// next iteration's four dwordx4 loads are issued before the current one is reduced.
+// ---- fast path: per-lane accumulation --------------------------------------------------
+// L in {64,128,256}; LPC = L/32 lanes per candidate, each streams 32 B of each row.  Per 4
+// bytes: S1 = sum x and S2 = sum x^2 by unsigned v_dot4, the shifted y = x-128 only for
+// y^3/y^4 (v_perm unpack, packed i16 sub/mul, v_dot2); branch-free finalisation with compile-time powers of 1/L (exact for
+// L = 2^k, so mean and m2..m4 are the correctly rounded rationals with no division).
 struct Acc2 {
   uint32_t s1, s2;
   int t3;
@@ -279,79 +176,8 @@ __device__ __forceinline__ void stats4(const Acc2& a, double (&st)[4]) {
   st[3] = zero ? __builtin_nan("") : m4 / (m2 * m2) - 3.0;
 }
 
-template <int L>
-__global__ __launch_bounds__(256) void lyon8_u8_fast2(const uint8_t* __restrict__ prof,
-                                                      int64_t ps,
-                                                      const uint8_t* __restrict__ dm,
-                                                      int64_t ds, int64_t n,
-                                                      double* __restrict__ out) {
-  constexpr int LPC = L / 32;
-  constexpr int CPW = 64 / LPC;
-  constexpr int SPL = 8 / LPC;
-  const int lane = threadIdx.x & 63;
-  const int sub = lane % LPC;
-  const int cw = lane / LPC;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * CPW;
-  auto load = [&](int64_t c, u32x4& p0, u32x4& p1, u32x4& d0, u32x4& d1) {
-    if (c < n) {
-      const u32x4* pp = reinterpret_cast<const u32x4*>(prof + c * ps + sub * 32);
-      const u32x4* dp = reinterpret_cast<const u32x4*>(dm + c * ds + sub * 32);
-      p0 = __builtin_nontemporal_load(pp);
-      p1 = __builtin_nontemporal_load(pp + 1);
-      d0 = __builtin_nontemporal_load(dp);
-      d1 = __builtin_nontemporal_load(dp + 1);
-    } else {
-      p0 = p1 = d0 = d1 = (u32x4){0, 0, 0, 0};
-    }
-  };
-  int64_t base = wave * CPW;
-  u32x4 p0, p1, d0, d1;
-  load(base + cw, p0, p1, d0, d1);
-  for (; base < n; base += stride) {
-    const int64_t c = base + cw;
-    u32x4 q0, q1, e0, e1;
-    load(c + stride, q0, q1, e0, e1);  // prefetch the next candidate of this lane group
-    Acc2 sp = {0, 0, 0, 0}, sd = {0, 0, 0, 0};
-    acc2_x4(p0, sp);
-    acc2_x4(p1, sp);
-    acc2_x4(d0, sd);
-    acc2_x4(d1, sd);
-    acc2_reduce<LPC>(sp);
-    acc2_reduce<LPC>(sd);
-    const int j0 = sub * SPL;
-    const bool is_dm = j0 >= 4;
-    Acc2 s;
-    s.s1 = is_dm ? sd.s1 : sp.s1;
-    s.s2 = is_dm ? sd.s2 : sp.s2;
-    s.t3 = is_dm ? sd.t3 : sp.t3;
-    s.t4 = is_dm ? sd.t4 : sp.t4;
-    double st[4];
-    stats4<L>(s, st);
-    if (c < n) {
-      double* o = out + c * 8 + j0;
-      if constexpr (SPL == 4) {
-        __builtin_nontemporal_store((f64x2){st[0], st[1]}, reinterpret_cast<f64x2*>(o));
-        __builtin_nontemporal_store((f64x2){st[2], st[3]}, reinterpret_cast<f64x2*>(o) + 1);
-      } else if constexpr (SPL == 2) {
-        const bool hi2 = (j0 & 3) != 0;
-        __builtin_nontemporal_store((f64x2){hi2 ? st[2] : st[0], hi2 ? st[3] : st[1]},
-                                    reinterpret_cast<f64x2*>(o));
-      } else {
-        const int k = j0 & 3;
-        const double v = k == 0 ? st[0] : k == 1 ? st[1] : k == 2 ? st[2] : st[3];
-        __builtin_nontemporal_store(v, o);
-      }
-    }
-    p0 = q0;
-    p1 = q1;
-    d0 = e0;
-    d1 = e1;
-  }
-}
-
-// ---- fast path, v3 -------------------------------------------------------------------
-// v2's arithmetic, but each wave step covers U consecutive groups of CPW candidates, so a
+// ---- fast path: the stream kernel ------------------------------------------------------
+// Each wave step covers U consecutive groups of CPW candidates, so a
 // wave reads U*CPW*L contiguous bytes of each input in one burst (8 KiB per array at
 // L = 128, U = 4: measured +5% HBM throughput over one group, tools/membw.hip), and all
 // 4*U dwordx4 loads are issued unconditionally (out-of-range groups re-read the last row)
@@ -506,14 +332,10 @@ __global__ __launch_bounds__(256) void lyon8_f64_generic(const double* __restric
 // ---- launchers (called from capi.cpp) ---------------------------------------------------
 namespace pfe {
 
-static inline int grid_for(int64_t work_waves) {
-  // 4 waves per block; cap at 256 CUs x 32 blocks (7 resident waves per SIMD at 71 VGPRs: +1-2 % over
-  // 8 blocks per CU, tools/ab_lyon8_grid.sh) and grid-stride the rest
-  // (PFE_LYON8_BLOCKS overrides the cap: A/B runs)
-  static const int64_t cap = [] {
-    const char* v = getenv("PFE_LYON8_BLOCKS");
-    return (int64_t)(v && atoi(v) > 0 ? atoi(v) : 8192);
-  }();
+static inline int grid_for(int64_t work_waves, int cap) {
+  // 4 waves per block; capped (handle option PFE_OPT_LYON8_BLOCKS, default 256 CUs x 32
+  // blocks: 7 resident waves per SIMD at 71 VGPRs, +1-2 % over 8 blocks per CU,
+  // tools/ab_lyon8_grid.sh) and grid-stride the rest
   int64_t blocks = (work_waves + 3) / 4;
   if (blocks < 1) blocks = 1;
   if (blocks > cap) blocks = cap;
@@ -521,28 +343,25 @@ static inline int grid_for(int64_t work_waves) {
 }
 
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
-                           int64_t ds, int ld, int64_t n, double* out, hipStream_t st) {
+                           int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
+                           const Options& o) {
   if (n <= 0) return hipSuccess;
   const bool aligned = ((uintptr_t)prof % 16 == 0) && ((uintptr_t)dm % 16 == 0) &&
                        (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  static const int variant = [] {
-    const char* v = getenv("PFE_LYON8_VARIANT");  // A/B switch for benchmarking only
-    return v ? atoi(v) : 32;
-  }();
-  if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256) && variant >= 31) {
-    const int U = variant - 30;  // 31 -> U=1, 32 -> U=2, 34 -> U=4
+  if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
+    const int U = o.lyon8_burst;  // 1, 2 (default) or 4 candidate groups per wave step
     const int cpw = 64 / (lp / 32) * U;
-    const int grid = grid_for((n + cpw - 1) / cpw);
+    const int grid = grid_for((n + cpw - 1) / cpw, o.lyon8_blocks);
 #define PFE_L8(LL, UU) \
   hipLaunchKernelGGL((lyon8_u8_fast3<LL, UU>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out)
 #define PFE_L8U(LL)          \
   do {                       \
     if (U == 1)              \
       PFE_L8(LL, 1);         \
-    else if (U == 2)         \
-      PFE_L8(LL, 2);         \
-    else                     \
+    else if (U == 4)         \
       PFE_L8(LL, 4);         \
+    else                     \
+      PFE_L8(LL, 2);         \
   } while (0)
     if (lp == 64)
       PFE_L8U(64);
@@ -552,35 +371,18 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
       PFE_L8U(256);
 #undef PFE_L8U
 #undef PFE_L8
-  } else if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256) && variant == 2) {
-    const int cpw = 64 / (lp / 32);
-    const int grid = grid_for((n + cpw - 1) / cpw);
-    if (lp == 64)
-      hipLaunchKernelGGL(lyon8_u8_fast2<64>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
-    else if (lp == 128)
-      hipLaunchKernelGGL(lyon8_u8_fast2<128>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
-    else
-      hipLaunchKernelGGL(lyon8_u8_fast2<256>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
-  } else if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
-    const int cpw = 64 / (lp / 32);
-    const int grid = grid_for((n + cpw - 1) / cpw);
-    if (lp == 64)
-      hipLaunchKernelGGL(lyon8_u8_fast<64>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
-    else if (lp == 128)
-      hipLaunchKernelGGL(lyon8_u8_fast<128>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
-    else
-      hipLaunchKernelGGL(lyon8_u8_fast<256>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out);
   } else {
-    const int grid = grid_for(2 * n);
+    const int grid = grid_for(2 * n, o.lyon8_blocks);
     hipLaunchKernelGGL(lyon8_u8_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_lyon8_f64(const double* prof, int64_t ps, int lp, const double* dm,
-                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st) {
+                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
+                            const Options& o) {
   if (n <= 0) return hipSuccess;
-  const int grid = grid_for(2 * n);
+  const int grid = grid_for(2 * n, o.lyon8_blocks);
   hipLaunchKernelGGL(lyon8_f64_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);
   return hipGetLastError();
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/pfe.h"
+#include "options.h"
 
 namespace pfe {
 
@@ -21,6 +22,7 @@ struct PfdArgs {
   // DM-fit inputs [period, snr, dm, width, dm_start, dm_end] into par22 (n x 8); both or none
   double* out22 = nullptr;
   double* par22 = nullptr;
+  int waves = 4;  // handle option PFE_OPT_PFD_WAVES: the four-wave kernel (<= 128 bins) or one wave
 };
 
 size_t pfd_lds_bytes(int nsub, int L);
@@ -29,6 +31,6 @@ hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st);
 size_t pfd22_workspace_bytes(int64_t n, int L);
 struct Fork;
 hipError_t launch_pfd22(PfdArgs a, double* out, uint32_t* status, void* work, size_t work_bytes,
-                        hipStream_t st, const Fork* fk);
+                        hipStream_t st, const Fork* fk, const Options& o);
 
 }  // namespace pfe

@@ -690,8 +690,7 @@ static size_t pfd4_lds_bytes(int nsub, int L) {
 }
 
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {
-  const char* e4 = getenv("PFE_PFD4");
-  if (a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && !(e4 && e4[0] == '0')) {
+  if (a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4) {
     const size_t lds4 = pfd4_lds_bytes(a.nsub, a.L);
     static size_t configured4 = 0;
     if (lds4 > 48 * 1024 && lds4 > configured4) {

@@ -22,7 +22,7 @@ namespace pfe {
 hipError_t launch_sine(const BatesArgs& a, hipStream_t st);
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
 size_t bates22_workspace_bytes(const pfe_bates_in* in);
-void bates_setup(BatesArgs& a, int64_t n, int lp, void* work);
+void bates_setup(BatesArgs& a, int64_t n, int lp, void* work, const Options& o);
 void launch_clear_internal(uint32_t* status, int64_t n, hipStream_t st);
 bool fork_begin(const Fork* fk, hipStream_t st);
 hipError_t fork_end(const Fork* fk, hipStream_t st);
@@ -339,7 +339,7 @@ static char* carve(char*& p, size_t bytes) {
 
 // pa: the PFD inputs (profs, subfreqs, scal, shape, n); out n x 22, status n (device)
 hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, size_t work_bytes,
-                        hipStream_t st, const Fork* fk) {
+                        hipStream_t st, const Fork* fk, const Options& o) {
   const int64_t n = pa.n;
   const int L = pa.L;
   if (work_bytes < pfd22_workspace_bytes(n, L)) return hipErrorInvalidValue;
@@ -358,7 +358,7 @@ hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, s
   pa.par22 = par22;
   if ((e = launch_pfd_dmprof(pa, st)) != hipSuccess) return e;
   BatesArgs a;
-  bates_setup(a, n, L, bwork);
+  bates_setup(a, n, L, bwork, o);
   a.prof = nullptr;
   a.fprof = profile;
   a.sub = nullptr;
@@ -375,9 +375,7 @@ hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, s
   const hipStream_t sg = forked ? fk->side[0] : st, sd = forked ? fk->side[1] : st;
   if ((e = launch_gauss(a, sg)) != hipSuccess) return e;
   const PfdDMArgs d{a, chis};
-  const char* g = getenv("PFE_GLM");
-  const char* b = getenv("PFE_BLM");
-  if (!(g && g[0] == '0') && !(b && b[0] == '0'))  // pooled group-LM unless an A/B run opts out
+  if (a.solver == PFE_SOLVER_POOLED)  // pooled group-LM unless the handle selects another solver
     hipLaunchKernelGGL((k_pfd_dmfitg<2>), dim3((unsigned)a.pwaves), dim3(64), 0, sd, d);
   else
     hipLaunchKernelGGL((k_pfd_dmfitb<2, BLM_FPW>), dim3((unsigned)((n + a.fpw - 1) / a.fpw)),

@@ -1,0 +1,420 @@
+// subband.hip — scores 20-22: the sub-band scores of a candidate.
+//
+// Reference: PHCXOperations.getSubbandParameters (PHCXOperations.py:305-349), which calls
+// ProfileOperations.getSubband_scores (ProfileOperations.py:1585-1686) and getProfileCorr
+// (PHCXOperations.py:387-415):
+//   s20  RMS scatter of the boxcar-maximum positions of the sub-bands, over the boxcar
+//        width wb = int(ceil(width * nBins))                     (:1603-1659, :1678)
+//   s21  mean numpy.corrcoef of every pair (i < k) of boxcar-sum vectors, NaN pairs
+//        skipped, ZeroDivisionError when none is left            (:1663-1675)
+//   s22  sum of |corrcoef(sub-band j, profile)| over the values > 0.0055 (:403-415, :345-347)
+//
+// Design (one wave per candidate, any nsub, nBins up to 1024):
+//   * The candidate's nsub x lsb sub-band bytes are read once (16 B per lane, coalesced) and
+//     turned into per-band exclusive prefix sums E[i][t] = sum_{u<t} x[i][u] in LDS (u16 up
+//     to 256 bins, else u32): a 16-byte piece is prefixed in the lane with v_dot4, the
+//     pieces of one band by a segmented lane scan.  Every boxcar sum is then
+//     b[i][j] = E[i][j+wb] - E[i][j] (two LDS reads) and every raw byte E[i][j+1] - E[i][j].
+//   * s20 and the maxima are integer-exact: the first strict maximum over j is the maximum
+//     of the 32-bit key (b << 10) | (1023 - j).
+//   * s21 without the nsub^2 pair loop: the boxcar sums are integers, so per band
+//     S = sum b and N = nw * sum b^2 - S^2 are exact, and z = (nw b - S) / sqrt(nw N) has
+//     <z_i, z_k> = corrcoef(b_i, b_k) (zero-variance bands, the reference's NaN pairs, are
+//     left out: N = 0 exactly when numpy's variance is 0).  Hence
+//         sum_{i<k} cc_ik = (sum_j (sum_i z_ij)^2 - sum_i |z_i|^2) / 2,
+//     over the m = v(v-1)/2 pairs of the v valid bands: O(nsub nw) work instead of
+//     O(nsub^2 nw).  It equals numpy's pair loop to rounding (~1e-15 relative; the parity
+//     bar for s21 is 1e-5).
+//   * s22 keeps numpy's arithmetic: centred fp64 values, per-lane partials over the slots in
+//     order and the fixed butterfly (wsum), which is bit-identical to the reference's
+//     corrcoef at 64/128/256 bins.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "../../include/pfe.h"
+#include "bates_common.h"
+#include "wave.h"
+
+namespace pfe {
+
+struct SubArgs {
+  const uint8_t* prof;  // n x lp
+  int lp;
+  const uint8_t* sub;   // n x nsub x lsb
+  int nsub, lsb;
+  const double* scal;   // n x PFE_NSCAL (width at PFE_SCAL_WIDTH)
+  int64_t n;
+  double* out;          // scores 20-22 of candidate c at out[c * ldo + 0..2]
+  int ldo;
+  uint32_t* status;
+};
+
+constexpr int SB_NB = 16;  // bands per register block
+
+// LDS row stride (elements) of the prefix array: 16-B aligned rows of lsb + 1 entries
+template <typename PT>
+__host__ __device__ constexpr int sb_stride(int lsb) {
+  return sizeof(PT) == 2 ? ((lsb + 1 + 7) & ~7) : ((lsb + 1 + 3) & ~3);
+}
+template <typename PT>
+__host__ __device__ constexpr size_t sb_wave_lds(int nsub, int lsb) {
+  return ((size_t)nsub * sb_stride<PT>(lsb) * sizeof(PT) + 15) / 16 * 16 + ((size_t)nsub * 4 + 15) / 16 * 16;
+}
+
+// 16 bytes -> their 16 exclusive prefixes (packed into the 8/16 dwords of a PT row piece)
+// plus the piece total
+__device__ __forceinline__ uint32_t piece_prefix(const uint32_t (&w)[4], uint32_t (&e)[16]) {
+  uint32_t run = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = w[d];
+    e[4 * d + 0] = run;
+    e[4 * d + 1] = run + __builtin_amdgcn_udot4(x, 0x00000001u, 0u, false);
+    e[4 * d + 2] = run + __builtin_amdgcn_udot4(x, 0x00000101u, 0u, false);
+    e[4 * d + 3] = run + __builtin_amdgcn_udot4(x, 0x00010101u, 0u, false);
+    run += __builtin_amdgcn_udot4(x, 0x01010101u, 0u, false);
+  }
+  return run;
+}
+
+// Fill E (this wave's prefix rows) for the fast layout: lsb a power of two in [16, 1024] and a
+// 16-B aligned block: pieces of 16 bytes never cross a band, a band is seg = lsb/16 lanes.
+template <typename PT>
+__device__ __forceinline__ void fill_prefix_fast(const uint8_t* sb, int nsub, int lsb, PT* E, int lane) {
+  const int stride = sb_stride<PT>(lsb);
+  const int seg = lsb >= 1024 ? 64 : lsb / 16;
+  const int64_t total = (int64_t)nsub * lsb;
+  for (int64_t base = 0; base < total; base += 1024) {
+    const int64_t off = base + 16 * lane;
+    const bool ok = off < total;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (ok) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sb + off));
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    }
+    uint32_t e[16];
+    const uint32_t tot = piece_prefix(w, e);
+    // exclusive scan of the piece totals inside the band's lane segment
+    uint32_t x = tot;
+    const int pos = lane & (seg - 1);
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      if (s >= seg) break;
+      const uint32_t o = (uint32_t)__shfl_up((int)x, s);
+      if (pos >= s) x += o;
+    }
+    const uint32_t excl = x - tot;
+    if (ok) {
+      const int band = (int)(off / lsb);
+      const int t0 = (int)(off - (int64_t)band * lsb);
+      PT* row = E + (size_t)band * stride + t0;
+      if constexpr (sizeof(PT) == 2) {
+        uint32_t pk[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pk[q] = ((e[2 * q] + excl) & 0xFFFFu) | ((e[2 * q + 1] + excl) << 16);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
+        reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
+      } else {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          reinterpret_cast<u32x4*>(row)[q] =
+              (u32x4){e[4 * q] + excl, e[4 * q + 1] + excl, e[4 * q + 2] + excl, e[4 * q + 3] + excl};
+      }
+      if (t0 + 16 == lsb) row[16] = (PT)(excl + tot);  // E[band][lsb]
+    }
+  }
+}
+
+// Fill E for any lsb / alignment: one band at a time, ceil(lsb/64) contiguous bytes per lane.
+template <typename PT>
+__device__ __forceinline__ void fill_prefix_generic(const uint8_t* sb, int nsub, int lsb, PT* E, int lane) {
+  const int stride = sb_stride<PT>(lsb);
+  const int ch = (lsb + 63) / 64;
+  for (int i = 0; i < nsub; ++i) {
+    const uint8_t* src = sb + (size_t)i * lsb;
+    const int t0 = lane * ch;
+    uint32_t run = 0;
+    for (int u = 0; u < ch; ++u)
+      if (t0 + u < lsb) run += src[t0 + u];
+    const uint32_t excl = (uint32_t)wscan_excl((int)run);
+    PT* row = E + (size_t)i * stride;
+    uint32_t acc = excl;
+    for (int u = 0; u < ch; ++u)
+      if (t0 + u < lsb) {
+        row[t0 + u] = (PT)acc;
+        acc += src[t0 + u];
+      }
+    if (t0 < lsb && t0 + ch >= lsb) row[lsb] = (PT)acc;
+  }
+}
+
+// numpy.corrcoef's off-diagonal entry from the centred sums (clip keeps NaN)
+__device__ __forceinline__ double sb_corr(double cxy, double cxx, double cyy) {
+  double r = (cxy / sqrt(cxx)) / sqrt(cyy);
+  if (r > 1.0) r = 1.0;
+  if (r < -1.0) r = -1.0;
+  return r;
+}
+
+// SL = ceil(lsb / 64) window / bin slots per lane; WPB waves (candidates) per block
+template <int SL, typename PT, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
+  extern __shared__ __align__(16) unsigned char sb_lds[];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * WPB + w;
+  if (c >= a.n) return;
+  const int nsub = a.nsub, lsb = a.lsb;
+  const size_t wave_bytes = sb_wave_lds<PT>(nsub, lsb);
+  PT* E = reinterpret_cast<PT*>(sb_lds + w * wave_bytes);
+  int* maxbin = reinterpret_cast<int*>(sb_lds + w * wave_bytes +
+                                       ((size_t)nsub * sb_stride<PT>(lsb) * sizeof(PT) + 15) / 16 * 16);
+  const int stride = sb_stride<PT>(lsb);
+
+  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
+  const double wbd = ceil(width * (double)lsb);                      // :1603
+  // wb <= 0: rms = stdev / 0 or no valid pair; wb > lsb: no window, max_bin unbound;
+  // lp != lsb: corrcoef of different lengths raises (:403)
+  if (!(wbd >= 1.0) || wbd > (double)lsb || a.lp != lsb) {
+    if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+    return;
+  }
+  const int wb = (int)wbd;
+  const int nw = lsb - wb + 1;                                        // windows per band
+  const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
+  const bool fast = ((lsb & (lsb - 1)) == 0) && lsb >= 16 && (((uintptr_t)sb & 15) == 0);
+  if (fast)
+    fill_prefix_fast<PT>(sb, nsub, lsb, E, lane);
+  else
+    fill_prefix_generic<PT>(sb, nsub, lsb, E, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // the profile, centred as numpy.corrcoef centres it (s22)
+  double pv[SL];
+  double pm = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    const int j = lane + 64 * k;
+    pv[k] = (j < lsb) ? (double)a.prof[c * a.lp + j] : 0.0;
+    pm += pv[k];
+  }
+  pm = wsum(pm) / (double)lsb;
+  double pvar = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    pv[k] = (lane + 64 * k < lsb) ? pv[k] - pm : 0.0;
+    pvar += pv[k] * pv[k];
+  }
+  pvar = wsum(pvar);
+  const double inv2 = 1.0 / (double)(lsb - 1);
+
+  const double dnw = (double)nw;
+  double Z[SL];      // sum over the valid bands of z_ij, window j = lane + 64k
+#pragma unroll
+  for (int k = 0; k < SL; ++k) Z[k] = 0.0;
+  double zz = 0.0;   // sum of z_ij^2
+  int valid = 0;     // bands with non-zero variance
+  double integ = 0.0;
+
+  for (int blk = 0; blk < nsub; blk += SB_NB) {
+    const int nb = nsub - blk < SB_NB ? nsub - blk : SB_NB;
+    // ---- boxcar statistics: S, sum b^2, first strict maximum -------------------------
+    long long S[SB_NB], Q[SB_NB];
+    int key[SB_NB];
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      long long s = 0, q = 0;
+      int kmax = 0;
+      if (ii < nb) {
+        const PT* row = E + (size_t)(blk + ii) * stride;
+#pragma unroll
+        for (int k = 0; k < SL; ++k) {
+          const int j = lane + 64 * k;
+          if (j < nw) {
+            const int b = (int)row[j + wb] - (int)row[j];
+            s += b;
+            q += (long long)b * b;
+            const int kk = (b << 10) | (1023 - j);
+            kmax = kk > kmax ? kk : kmax;
+          }
+        }
+      }
+      S[ii] = s;
+      Q[ii] = q;
+      key[ii] = kmax;
+    }
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      S[ii] = wsum_ll(S[ii]);
+      Q[ii] = wsum_ll(Q[ii]);
+      key[ii] = wmax_i(key[ii]);
+    }
+    double r[SB_NB];
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      const long long N = (long long)nw * Q[ii] - S[ii] * S[ii];  // exact: nw^2 var(b)
+      r[ii] = (ii < nb && N > 0) ? 1.0 / sqrt(dnw * (double)N) : 0.0;
+      valid += (ii < nb && N > 0) ? 1 : 0;
+      if (ii < nb && lane == 0) maxbin[blk + ii] = 1023 - (key[ii] & 1023) + wb / 2;  // :1628
+    }
+    // ---- z-scores of the valid bands; centred bytes against the profile ---------------
+    double sv[SB_NB], d[SB_NB];
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      int bs = 0;
+      if (ii < nb) {
+        const PT* row = E + (size_t)(blk + ii) * stride;
+        bs = (int)row[lsb];
+#pragma unroll
+        for (int k = 0; k < SL; ++k) {
+          const int j = lane + 64 * k;
+          if (j < nw && r[ii] != 0.0) {
+            const int b = (int)row[j + wb] - (int)row[j];
+            const double z = (double)((long long)nw * b - S[ii]) * r[ii];
+            Z[k] += z;
+            zz += z * z;
+          }
+        }
+      }
+      // numpy: mu = mean(sub_j); t = sub_j - mu; d = sum t * pv; q = sum t^2 (per-lane slots
+      // in order, then the fixed butterfly)
+      const double mu = (double)bs / (double)lsb;
+      double dd = 0.0, q = 0.0;
+      if (ii < nb) {
+        const PT* row = E + (size_t)(blk + ii) * stride;
+#pragma unroll
+        for (int k = 0; k < SL; ++k) {
+          const int j = lane + 64 * k;
+          if (j < lsb) {
+            const double t = (double)((int)row[j + 1] - (int)row[j]) - mu;
+            dd += t * pv[k];
+            q += t * t;
+          }
+        }
+      }
+      sv[ii] = q;
+      d[ii] = dd;
+    }
+    wsum_arr(sv);
+    wsum_arr(d);
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      if (ii < nb) {
+        const double cc = fabs(sb_corr(d[ii] * inv2, sv[ii] * inv2, pvar * inv2));
+        if (cc > 0.0055) integ += cc;                                 // in band order
+      }
+    }
+  }
+  // ---- s21 -----------------------------------------------------------------------------
+  double zs = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) zs += Z[k] * Z[k];
+  zs = wsum(zs);
+  zz = wsum(zz);
+  const long long m = (long long)valid * (valid - 1) / 2;
+  if (m == 0) {  // ZeroDivisionError (:1681)
+    if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+    return;
+  }
+  const double mean_corr = (0.5 * (zs - zz)) / (double)m;
+  // ---- s20: RMS scatter of the maxima (:1633-1659, :1678) --------------------------------
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double msum = 0.0;
+  for (int i = 0; i < nsub; ++i) msum += (double)maxbin[i];
+  const double med = msum / (double)nsub;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i = 0; i < nsub; ++i) {
+    const double v = (double)maxbin[i];
+    if (fabs(v - med) <= (double)wb) {
+      ++count;
+      var_med += (v - med) * (v - med);
+    }
+  }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    double mu = 0.0;
+    for (int i = 0; i < nsub; ++i) mu += (double)maxbin[i];
+    mu /= (double)nsub;
+    var = 0.0;
+    for (int i = 0; i < nsub; ++i) var += ((double)maxbin[i] - mu) * ((double)maxbin[i] - mu);
+    var /= (double)(nsub - 1);
+  }
+  const double rms = sqrt(var) / (double)wb;
+  if (lane == 0) {
+    double* o = a.out + c * a.ldo;
+    o[0] = rms;
+    o[1] = mean_corr;
+    o[2] = integ;
+  }
+}
+
+// ---- launchers -------------------------------------------------------------------------
+// nullptr when the shape is scored, else why not (checked by the C-ABI before any launch)
+const char* subband_shape_error(int nsub, int lsb) {
+  if (nsub < 2 || nsub > 256) return "nsub outside [2, 256]";
+  if (lsb < 1 || lsb > 1024) return "lsb outside [1, 1024]";
+  if ((int64_t)nsub * (lsb + 1) > 32768) return "nsub * (lsb + 1) exceeds 32768 (LDS-resident limit)";
+  return nullptr;
+}
+
+template <int SL, typename PT>
+static hipError_t launch_sl(const SubArgs& s, hipStream_t st) {
+  const size_t wave = sb_wave_lds<PT>(s.nsub, s.lsb);
+  if (wave * 4 <= 40 * 1024) {
+    hipLaunchKernelGGL((k_subband2<SL, PT, 4>), dim3((unsigned)((s.n + 3) / 4)), dim3(256),
+                       wave * 4, st, s);
+  } else {
+    static size_t configured = 0;
+    if (wave > 48 * 1024 && wave > configured) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_subband2<SL, PT, 1>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave);
+      if (e != hipSuccess) return e;
+      configured = wave;
+    }
+    hipLaunchKernelGGL((k_subband2<SL, PT, 1>), dim3((unsigned)s.n), dim3(64), wave, st, s);
+  }
+  return hipGetLastError();
+}
+
+static hipError_t launch_sub(const SubArgs& s, hipStream_t st) {
+  if (s.n <= 0) return hipSuccess;
+  if (subband_shape_error(s.nsub, s.lsb)) return hipErrorInvalidValue;
+  const int L = s.lsb;
+  if (L <= 64) return launch_sl<1, uint16_t>(s, st);
+  if (L <= 128) return launch_sl<2, uint16_t>(s, st);
+  if (L <= 256) return launch_sl<4, uint16_t>(s, st);
+  if (L <= 512) return launch_sl<8, uint32_t>(s, st);
+  return launch_sl<16, uint32_t>(s, st);
+}
+
+// the 22-score chain: scores 20-22 into columns 19-21 of out (n x 22)
+hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
+  SubArgs s{a.prof, a.lp, a.sub, a.nsub, a.lsb, a.scal, a.n, a.out + 19, 22, a.status};
+  return launch_sub(s, st);
+}
+
+// pfe_subband3: out n x 3; status zeroed here
+hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(status, 0, (size_t)in->n * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(out, 0, (size_t)in->n * 3 * sizeof(double), st);
+  if (e != hipSuccess) return e;
+  SubArgs s{in->prof, in->lp, in->sub, in->nsub, in->lsb, in->scal, in->n, out, 3, status};
+  return launch_sub(s, st);
+}
+
+}  // namespace pfe

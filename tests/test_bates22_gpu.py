@@ -1,16 +1,22 @@
 """GPU parity of pfe_bates22 (C-ABI) against the reference's golden vectors and the oracle.
 
-Bar (SURVEY.md §8(a) parity classes; DESIGN.md §Parity):
+Bar (SURVEY.md §8(a) parity classes; DESIGN.md §4):
   * the failing candidates (reference raised -> row dropped) are exactly the same;
   * s3 (integer peak count), s4, s12-s16, s20, s22: bit-exact on every candidate;
-  * every other score j: the fraction of candidates where GPU and reference differ by more
-    than 1e-5 (and 1e-3) relative is at most 1.5 x the reference's own chaos floor + 3%,
-    where the floor is the fraction of candidates whose score moves when every leastsq
-    start point of the REFERENCE is nudged by one ulp (tests/golden/chaos_floor.json,
-    tools/chaos_floor.py).  For the well-conditioned scores (s1, s2, s19, s21; floor ~0)
-    that means >= 97% within 1e-5; for the ill-conditioned LM outputs (s8, s10, s11, s17,
-    s18: floors 20-60%) the GPU is held to "indistinguishable from a 1-ulp perturbation of
-    the reference".
+  * every other score j (the class-X fits s1, s2, s19, s21 included) but s10/s11, row by
+    row against the golden sets: on every candidate whose
+    reference score is stable -- it moves by at most STABLE relative under each of three
+    1-ulp-scale nudges of every leastsq start point (tests/golden/chaos_rows.npz,
+    tools/chaos_rows.py) -- the GPU is within 1e-5 of the reference; on the candidates
+    where the reference itself moves, the GPU may differ, and the fraction of candidates
+    differing by more than 1e-5 (1e-3) is held to 1.5 x the reference's own floor (the
+    fraction of candidates moving under the nudges, tests/golden/chaos_floor.json and
+    chaos_rows.npz) plus one candidate;
+  * s10/s11 (the 8-pass double-Gaussian peel) are held to the population floor only: the
+    reference does not reproduce ITSELF there -- the same candidate scored twice in one
+    process moves s10/s11 in 4-18% of rows (tests/test_oracle_golden.py) --
+    so a golden value of a candidate that is stable under the nudges is still not a pin;
+  * fresh (non-golden) batches are checked against the oracle with that batch's own floor.
 """
 import json
 import os
@@ -18,14 +24,16 @@ import os
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN, bates_inputs, load, oracle_with_floor
+from golden_util import GOLDEN, SELF_NOISY, bates_inputs, load, oracle_with_floor
 from oracle.bates import bates22 as oracle_bates22
 from pulsarfeatureextractor_amd.synth import bates_batch
 
 pytestmark = pytest.mark.gpu
 
 BITEXACT = (2, 3, 11, 12, 13, 14, 15, 19, 21)
+STABLE = 1e-6                     # a reference score moving by <= this under the nudges is stable
 FLOOR = json.load(open(os.path.join(GOLDEN, "chaos_floor.json")))
+ROWS = np.load(os.path.join(GOLDEN, "chaos_rows.npz"))
 
 
 def rel_err(got, ref):
@@ -37,24 +45,34 @@ def rel_err(got, ref):
     return r
 
 
-def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(), slack=0.03):
-    """close: scores held to <= 1e-12 relative (class X) instead of bit-exactness -- s20/s22
-    at lengths where numpy's BLAS dot products sum in another order than a power-of-two
-    tree (the difference is an ulp)."""
+def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(), rmax=None):
+    """close: scores held to <= 1e-12 relative instead of bit-exactness -- s20/s22 at lengths
+    where numpy's BLAS dot products sum in another order than a power-of-two tree (the
+    difference is an ulp).  rmax: (n, 22) per-candidate reference movement under the
+    start-point nudges (golden sets): row-conditioned parity on the stable candidates."""
     gok = (st & 0xFF) == 0
     assert np.array_equal(gok, ref_ok), f"{tag}: failure pattern differs"
     got, ref = out[gok], ref[gok]
     r = rel_err(got, ref)
+    n = max(1, len(r))
     for j in bitexact:
         assert (r[:, j] == 0).all(), f"{tag}: s{j + 1} not bit-exact ({(r[:, j] > 0).sum()} rows)"
     for j in close:
         assert (r[:, j] <= 1e-12).all(), f"{tag}: s{j + 1} max rel {r[:, j].max():.3g} > 1e-12"
+    stable = None if rmax is None else rmax[gok] <= STABLE
+    if rmax is not None:  # the set's own floor over all the nudges, where it is larger
+        floor = {key: np.maximum(floor[key], (rmax[gok] > tol).mean(axis=0)).tolist()
+                 for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3"))}
     for j in range(22):
         if j in bitexact or j in close:
             continue
+        if stable is not None and j not in SELF_NOISY:
+            bad = np.where(stable[:, j] & (r[:, j] > 1e-5))[0]
+            assert len(bad) == 0, (f"{tag}: s{j + 1} beyond 1e-5 on {len(bad)} candidates where "
+                                   f"the reference is stable (rows {bad[:10].tolist()})")
         for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3")):
             moved = (r[:, j] > tol).mean()
-            allowed = 1.5 * floor[key][j] + slack
+            allowed = 1.5 * floor[key][j] + 1.0 / n
             assert moved <= allowed, (f"{tag}: s{j + 1} differs by > {tol} in {moved:.3f} of rows "
                                       f"(reference 1-ulp floor {floor[key][j]:.3f})")
 
@@ -64,7 +82,7 @@ def test_vs_reference_golden(engine, name):
     d = load(name)
     prof, sub, curve, scal = bates_inputs(d)
     out, st = engine.bates22(prof, sub, curve, scal)
-    check_against(out, st, d["out"], d["ok"], name, FLOOR[name])
+    check_against(out, st, d["out"], d["ok"], name, FLOOR[name], rmax=ROWS[f"{name}_rmax"])
 
 
 def test_vs_oracle_fresh_inputs(engine):
@@ -90,31 +108,28 @@ def test_vs_oracle_other_lengths(engine, lp, n):
                   bitexact=exact, close=() if pow2 else (19, 21))
 
 
-def test_batched_solver_bit_identical(engine, monkeypatch):
+def test_batched_solver_bit_identical(engine):
     """The batched lmdif kernels (lm_batch.h) reproduce the wave-per-fit kernels bit for bit
-    (PFE_BLM=0 selects the latter; PFE_GLM=0 keeps the pooled group kernels out)."""
+    (handle option solver = wave / batched)."""
     b = bates_batch(200, seed=21)
-    monkeypatch.setenv("PFE_GLM", "0")
-    monkeypatch.setenv("PFE_BLM", "0")
-    o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    monkeypatch.setenv("PFE_BLM", "1")
-    o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    with engine.options(solver="wave"):
+        o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    with engine.options(solver="batched"):
+        o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     assert np.array_equal(s0, s1)
     assert np.array_equal(np.nan_to_num(o0, nan=7.0), np.nan_to_num(o1, nan=7.0))
 
 
-def test_concurrent_groups_and_hand_over_bit_identical(engine, monkeypatch):
-    """The score groups on side streams (default) vs in order on one stream (PFE_SERIAL=1),
-    and the LM hand-over of accepted residuals (default) vs re-evaluation (PFE_HAND=0): the
-    same bits (tests/test_pfd22_gpu.py checks the PFD path)."""
+def test_concurrent_groups_and_hand_over_bit_identical(engine):
+    """The score groups on side streams (default) vs in order on one stream (option
+    serial=1), the LM hand-over of accepted residuals (default) vs re-evaluation
+    (handover=0), and the pool size (gslots): the same bits (tests/test_pfd22_gpu.py checks
+    the PFD path)."""
     b = bates_batch(300, seed=33)
     ref = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    for env in ({"PFE_SERIAL": "1"}, {"PFE_HAND": "0"}, {"PFE_SERIAL": "1", "PFE_HAND": "0"}):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        o, s = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-        for k in env:
-            monkeypatch.delenv(k)
+    for env in ({"serial": 1}, {"handover": 0}, {"serial": 1, "handover": 0}, {"gslots": 7}):
+        with engine.options(**env):
+            o, s = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
         assert np.array_equal(s, ref[1]), env
         assert np.array_equal(np.nan_to_num(o, nan=7.0), np.nan_to_num(ref[0], nan=7.0)), env
 
@@ -145,15 +160,14 @@ def test_batch_independence(engine):
 
 
 @pytest.mark.parametrize("lp", [128, 64])
-def test_pooled_group_solver(engine, monkeypatch, lp):
+def test_pooled_group_solver(engine, lp):
     """The pooled group-LM kernels (lm_group.h, the default for <= 128 bins) against the
     batched wave kernels: same failures, bit-exact columns identical, the LM outputs
     different only in the last bits of their m-sums (so at most at the reference's own
     1-ulp chaos rates), and every fit's result independent of the pool it ran in."""
     b = bates_batch(600, lp=lp, lsb=lp, seed=33 + lp)
-    monkeypatch.setenv("PFE_GLM", "0")
-    o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    monkeypatch.setenv("PFE_GLM", "1")
+    with engine.options(solver="batched"):
+        o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     assert np.array_equal(s0, s1)
     ok = (s0 & 0xFF) == 0

@@ -51,3 +51,49 @@ def test_bates22_oracle_vs_reference(name, rows):
             assert close[:, j].mean() >= 0.70, f"s{j + 1}: {close[:, j].mean():.3f}"
         else:
             assert same[:, j].all(), f"s{j + 1} not bit-exact in {(~same[:, j]).sum()} rows"
+
+
+def test_bates22_oracle_vs_reference_nsub32():
+    """32 sub-bands per candidate (nSub from the file)."""
+    d = load("bates22_phcx128_nsub32")
+    prof, sub, curve, scal = bates_inputs(d)
+    sel = np.arange(30)
+    out, st = bates22(prof[sel], sub[sel], curve[sel], scal[sel])
+    ok = d["ok"][sel]
+    assert np.array_equal((st & 0xFF) == 0, ok)
+    ref = d["out"][sel][ok]
+    got = out[ok]
+    for j in (19, 20, 21):
+        assert np.array_equal(got[:, j], ref[:, j]), f"s{j + 1}"
+
+
+def test_config4_literal_shape_oracle_fails_like_reference():
+    """256-bin profile with 16 x 128 sub-bands: every candidate fails (sub-band group, or the
+    Gaussian group first on the constant-profile row)."""
+    d = load("bates22_cfg4_256x128")
+    prof, sub, curve, scal = bates_inputs(d)
+    sel = np.arange(8)
+    out, st = bates22(prof[sel], sub[sel], curve[sel], scal[sel])
+    assert not d["ok"][sel].any()
+    gauss = np.array(["Gaussian" in e for e in d["err"][sel]])
+    assert np.array_equal((st & 0xFF) == 0x02, gauss)
+    assert ((st & 0xFF)[~gauss] == 0x08).all()
+
+
+def test_all30_oracle_vs_reference():
+    """Config 5's 30 values: Lyon features of the profile + section-0 DataBlock, then the 22
+    scores of the same file."""
+    d = load("all30_phcx128")
+    prof, sub, curve, scal = bates_inputs(d)
+    sel = np.arange(20)
+    l8 = lyon8(prof[sel], d["block0"][sel])
+    out, st = bates22(prof[sel], sub[sel], curve[sel], scal[sel])
+    ok = d["ok"][sel]
+    assert np.array_equal((st & 0xFF) == 0, ok)
+    ref = d["out"][sel][ok]
+    assert np.array_equal(l8[ok], ref[:, :8])
+    for j in range(22):
+        if j not in SELF_NOISY:
+            g, r = out[ok][:, j], ref[:, 8 + j]
+            assert np.array_equal(g, r) or np.array_equal(np.isnan(g), np.isnan(r)) and \
+                np.array_equal(g[~np.isnan(g)], r[~np.isnan(r)]), f"s{j + 1}"

@@ -125,16 +125,16 @@ def test_vs_oracle_fresh_shapes(engine, tmp_path, npart, nsub, L, n):
     check(out, st, ref, ok, f"oracle {npart}x{nsub}x{L}", floor)
 
 
-def test_concurrent_groups_and_hand_over_bit_identical(engine, tmp_path, monkeypatch):
-    """Side-stream score groups vs one stream (PFE_SERIAL=1), hand-over vs re-evaluation
-    (PFE_HAND=0): the same bits on the PFD path."""
+def test_concurrent_groups_and_hand_over_bit_identical(engine, tmp_path):
+    """Side-stream score groups vs one stream (option serial=1), hand-over vs re-evaluation
+    (handover=0), the single-wave preprocessing kernel (pfd_waves=1): the same bits on the
+    PFD path."""
     g = load_set(SETS[0])
     files = build_files(tmp_path, g)
     profs, sf, sc = pfd.batch_inputs([pfd.read(f) for f in files])
     ref, rst = engine.pfd_bates22(profs, sf, sc)
-    monkeypatch.setenv("PFE_SERIAL", "1")
-    monkeypatch.setenv("PFE_HAND", "0")
-    o, s = engine.pfd_bates22(profs, sf, sc)
+    with engine.options(serial=1, handover=0, pfd_waves=1):
+        o, s = engine.pfd_bates22(profs, sf, sc)
     assert np.array_equal(s, rst)
     assert np.array_equal(np.nan_to_num(o, nan=7.0), np.nan_to_num(ref, nan=7.0))
 

@@ -103,6 +103,11 @@ for f in files:
             v = [float(x) for x in a + b]
         elif mode == "profile":
             v = [float(x) for x in c.calculateProfileScores(False)]
+        elif mode == "all30":
+            a = list(c.calculateProfileStatScores(False))
+            b = list(c.calculateDMCurveStatScores(False))
+            v = [float(x) for x in a + b]
+            v += [float(x) for x in Candidate.Candidate(f, f).calculateScores(False)]
         else:
             v = [float(x) for x in c.calculateScores(False)]
         res.append({"ok": True, "v": v})
@@ -222,26 +227,41 @@ def collect(res, nout):
     return out, ok, np.array(errs)
 
 
-def main():
+SPECS = [
+    # name, mode, superb, n, lp, l0 (Lyon DM length), nsub, lsb, ndm, seed
+    ("lyon8_superb64", "lyon8", True, 400, 64, 64, 16, 64, 2, 1),
+    ("lyon8_phcx128", "lyon8", False, 400, 128, 128, 16, 128, 2, 2),
+    ("lyon8_phcx128_dmplane", "lyon8", False, 60, 128, 120 * 128, 16, 128, 2, 3),
+    ("bates22_phcx128", "bates22", False, 300, 128, 128, 16, 128, 128, 4),
+    ("bates22_superb64", "bates22", True, 150, 64, 64, 16, 64, 120, 5),
+    # config 4 as BASELINE.json words it (256-bin profile, 16 x 128 sub-bands): the
+    # reference's corrcoef of a 128-bin band with the 256-bin profile raises ValueError
+    ("bates22_cfg4_256x128", "bates22", False, 40, 256, 128, 16, 128, 128, 6),
+    # 32 sub-bands (nSub is read from the file, PHCXOperations.py:330-338)
+    ("bates22_phcx128_nsub32", "bates22", False, 60, 128, 128, 32, 128, 128, 7),
+    # config 5's 30-column matrix: 8 Lyon features then the 22 scores of the same files
+    ("all30_phcx128", "all30", False, 80, 128, 128, 16, 128, 128, 8),
+]
+
+
+def main(only=None):
     import scipy
 
     os.makedirs(GOLDEN, exist_ok=True)
-    manifest = {"numpy": np.__version__, "scipy": scipy.__version__,
-                "python": sys.version.split()[0], "reference": REF_SRC,
-                "patches": {k: [a for a, _ in v] for k, v in PATCHES.items()},
-                "lib2to3_fixers": ["print", "except", "has_key", "long", "numliterals"],
-                "sets": {}}
+    mpath = os.path.join(GOLDEN, "manifest.json")
+    if only and os.path.exists(mpath):
+        manifest = json.load(open(mpath))
+    else:
+        manifest = {"numpy": np.__version__, "scipy": scipy.__version__,
+                    "python": sys.version.split()[0], "reference": REF_SRC,
+                    "patches": {k: [a for a, _ in v] for k, v in PATCHES.items()},
+                    "lib2to3_fixers": ["print", "except", "has_key", "long", "numliterals"],
+                    "sets": {}}
     with tempfile.TemporaryDirectory(prefix="pfe_golden_") as tmp:
         refdir = build_reference(tmp)
-        specs = [
-            # name, mode, superb, n, lp, l0 (Lyon DM length), nsub, lsb, ndm, seed
-            ("lyon8_superb64", "lyon8", True, 400, 64, 64, 16, 64, 2, 1),
-            ("lyon8_phcx128", "lyon8", False, 400, 128, 128, 16, 128, 2, 2),
-            ("lyon8_phcx128_dmplane", "lyon8", False, 60, 128, 120 * 128, 16, 128, 2, 3),
-            ("bates22_phcx128", "bates22", False, 300, 128, 128, 16, 128, 128, 4),
-            ("bates22_superb64", "bates22", True, 150, 64, 64, 16, 64, 120, 5),
-        ]
-        for name, mode, superb, n, lp, l0, nsub, lsb, ndm, seed in specs:
+        for name, mode, superb, n, lp, l0, nsub, lsb, ndm, seed in SPECS:
+            if only and name not in only:
+                continue
             rng = np.random.default_rng(20261015 + 100 * seed)
             if mode == "lyon8":
                 prof, dm0 = lyon_set(rng, n, lp, l0, superb)
@@ -264,7 +284,7 @@ def main():
                               dm_start=0.0, dm_end=200.0, n_dm_index=101)
             files = write_files(os.path.join(tmp, name), name, arrays, superb)
             res = run_reference(refdir, files, mode, tmp)
-            nout = 8 if mode == "lyon8" else 22
+            nout = {"lyon8": 8, "bates22": 22, "all30": 30}[mode]
             out, ok, errs = collect(res, nout)
             np.savez_compressed(
                 os.path.join(GOLDEN, name + ".npz"),
@@ -279,7 +299,7 @@ def main():
                                       "seed": 20261015 + 100 * seed,
                                       "failures": int((~ok).sum())}
             print(f"{name}: {n} candidates, {int((~ok).sum())} reference failures", flush=True)
-    with open(os.path.join(GOLDEN, "manifest.json"), "w") as f:
+    with open(mpath, "w") as f:
         json.dump(manifest, f, indent=1)
 
 
@@ -359,5 +379,7 @@ if __name__ == "__main__":
         make_pfd_golden(man)
         with open(mpath, "w") as f:
             json.dump(man, f, indent=1)
+    elif "--only" in sys.argv:  # regenerate the named PHCX sets only, keep the others
+        main(set(sys.argv[sys.argv.index("--only") + 1].split(",")))
     else:
         main()
