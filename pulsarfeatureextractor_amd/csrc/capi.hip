@@ -35,7 +35,7 @@ const char* subband_shape_error(int nsub, int lsb);
 
 // chunked host path: device/staging slots in flight (H2D of k+1 | kernel k | D2H of k-1)
 constexpr int PIPE_SLOTS = 3;
-constexpr size_t PIPE_CHUNK_BYTES = 32u << 20;  // input bytes per chunk
+constexpr size_t PIPE_CHUNK_BYTES = 64u << 20;  // input bytes per chunk
 
 struct pfe_handle {
   int device = -1;
@@ -382,13 +382,19 @@ static int lyon8_host(pfe_handle* h, const T* prof, int64_t ps, int32_t lp, cons
     }
     if (!pin_p) pack_rows((T*)hslot, prof, ps, lp, r0, rows);
     if (!pin_d) pack_rows((T*)(hslot + pb), dm, ds, ld, r0, rows);
-    if (pin_p)
+    if (pin_p && ps == lp)
+      PFE_HIP(h, hipMemcpyAsync(dprof, prof + r0 * ps, (size_t)rows * lp * sizeof(T),
+                                hipMemcpyHostToDevice, h->h2d));
+    else if (pin_p)
       PFE_HIP(h, hipMemcpy2DAsync(dprof, lp * sizeof(T), prof + r0 * ps, ps * sizeof(T),
                                   lp * sizeof(T), rows, hipMemcpyHostToDevice, h->h2d));
     else
       PFE_HIP(h, hipMemcpyAsync(dprof, hslot, (size_t)rows * lp * sizeof(T),
                                 hipMemcpyHostToDevice, h->h2d));
-    if (pin_d)
+    if (pin_d && ds == ld)
+      PFE_HIP(h, hipMemcpyAsync(ddm, dm + r0 * ds, (size_t)rows * ld * sizeof(T),
+                                hipMemcpyHostToDevice, h->h2d));
+    else if (pin_d)
       PFE_HIP(h, hipMemcpy2DAsync(ddm, ld * sizeof(T), dm + r0 * ds, ds * sizeof(T),
                                   ld * sizeof(T), rows, hipMemcpyHostToDevice, h->h2d));
     else

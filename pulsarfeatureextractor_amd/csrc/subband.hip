@@ -163,6 +163,40 @@ __device__ __forceinline__ double sb_corr(double cxy, double cxx, double cyy) {
   return r;
 }
 
+// s20: RMS scatter of the boxcar-maximum positions (:1633-1659, :1678); wave-uniform
+__device__ __forceinline__ double rms_of_maxbins(const int* maxbin, int nsub, int wb) {
+  double msum = 0.0;
+  for (int i = 0; i < nsub; ++i) msum += (double)maxbin[i];
+  const double med = msum / (double)nsub;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i = 0; i < nsub; ++i) {
+    const double v = (double)maxbin[i];
+    if (fabs(v - med) <= (double)wb) {
+      ++count;
+      var_med += (v - med) * (v - med);
+    }
+  }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    double mu = 0.0;
+    for (int i = 0; i < nsub; ++i) mu += (double)maxbin[i];
+    mu /= (double)nsub;
+    var = 0.0;
+    for (int i = 0; i < nsub; ++i) var += ((double)maxbin[i] - mu) * ((double)maxbin[i] - mu);
+    var /= (double)(nsub - 1);
+  }
+  return sqrt(var) / (double)wb;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // SL = ceil(lsb / 64) window / bin slots per lane; WPB waves (candidates) per block
 template <int SL, typename PT, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
@@ -326,34 +360,264 @@ __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
     return;
   }
   const double mean_corr = (0.5 * (zs - zz)) / (double)m;
-  // ---- s20: RMS scatter of the maxima (:1633-1659, :1678) --------------------------------
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double msum = 0.0;
-  for (int i = 0; i < nsub; ++i) msum += (double)maxbin[i];
-  const double med = msum / (double)nsub;
-  int count = 0;
-  double var_med = 0.0;
-  for (int i = 0; i < nsub; ++i) {
-    const double v = (double)maxbin[i];
-    if (fabs(v - med) <= (double)wb) {
-      ++count;
-      var_med += (v - med) * (v - med);
+  // ---- s20 ------------------------------------------------------------------------------
+  wave_lds_sync();
+  const double rms = rms_of_maxbins(maxbin, nsub, wb);
+  if (lane == 0) {
+    double* o = a.out + c * a.ldo;
+    o[0] = rms;
+    o[1] = mean_corr;
+    o[2] = integ;
+  }
+}
+
+// ---- fast path: power-of-two nBins in [16, 256], 16-B aligned rows ---------------------
+// Every sum the three scores need is an exact integer here, so the kernel works in integers
+// and packed byte dot products and still returns numpy's bits:
+//   * s22: with L a power of two, mu = T/L and pm = P/L are exact, every centred product
+//     (x - mu)(p - pm) = (Lx - T)(Lp - P)/L^2 is exact and so is every partial sum, whatever
+//     the order -- numpy's d = sum (x-mu)(p-pm) equals (L XP - T P)/L exactly, with
+//     XP = sum x p, T = sum x, P = sum p (likewise sum (x-mu)^2 and the profile's): three
+//     v_dot4 sums per 16-byte piece, taken in the same pass that builds the prefix sums;
+//   * s20 / s21: boxcar sums and their S, sum b^2 in integers; per-band reductions are
+//     reduce-scatters (16 bands over the 16 lanes of a row: 15 exchanges instead of 16 x 6);
+//     the s21 identity of k_subband2 with W_j = sum_i r_i b_ij accumulated by fma.
+template <int LSB>
+__host__ __device__ constexpr size_t fast_wave_lds(int nsub) {
+  return ((size_t)nsub * sb_stride<uint16_t>(LSB) * 2 + 15) / 16 * 16 +
+         ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16;
+}
+
+template <int M>
+__device__ __forceinline__ int xor_i32(int v) {
+  if constexpr (M == 1)
+    return dpp_i32<DPP_QUAD_XOR1>(v);
+  else if constexpr (M == 2)
+    return dpp_i32<DPP_QUAD_XOR2>(v);
+  else
+    return __shfl_xor(v, M);
+}
+template <int M>
+__device__ __forceinline__ unsigned long long xor_u64(unsigned long long v) {
+  const int lo = xor_i32<M>((int)(uint32_t)v);
+  const int hi = xor_i32<M>((int)(uint32_t)(v >> 32));
+  return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int M>
+__device__ __forceinline__ int xor_v(int v) { return xor_i32<M>(v); }
+template <int M>
+__device__ __forceinline__ unsigned long long xor_v(unsigned long long v) { return xor_u64<M>(v); }
+
+// one reduce-scatter step: lanes with bit M keep the upper H entries, the others the lower
+template <int M, int H, typename T, typename Op>
+__device__ __forceinline__ void rs_step(T (&v)[16], int lane, Op op) {
+  const bool hi = (lane & M) != 0;
+#pragma unroll
+  for (int t = 0; t < H; ++t) {
+    const T keep = hi ? v[t + H] : v[t];
+    const T send = hi ? v[t] : v[t + H];
+    v[t] = op(keep, xor_v<M>(send));
+  }
+}
+// 16 per-lane values -> v[0] of lane l = the wave total of entry bitrev4(l & 15)
+template <typename T, typename Op>
+__device__ __forceinline__ void reduce_scatter16(T (&v)[16], int lane, Op op) {
+  rs_step<1, 8>(v, lane, op);
+  rs_step<2, 4>(v, lane, op);
+  rs_step<4, 2>(v, lane, op);
+  rs_step<8, 1>(v, lane, op);
+  v[0] = op(v[0], xor_v<16>(v[0]));
+  v[0] = op(v[0], xor_v<32>(v[0]));
+}
+__device__ __forceinline__ int bitrev4(int l) {
+  return ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
+}
+
+template <int LSB, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
+  constexpr int SL = LSB >= 64 ? LSB / 64 : 1;  // window slots per lane
+  constexpr int SEG = LSB / 16;                 // lanes per band in the 16-byte piece layout
+  constexpr int STRIDE = sb_stride<uint16_t>(LSB);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __align__(16) unsigned char sb_lds[];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * WPB + w;
+  if (c >= a.n) return;
+  const int nsub = a.nsub;
+  unsigned char* wbase = sb_lds + w * fast_wave_lds<LSB>(nsub);
+  uint16_t* E = reinterpret_cast<uint16_t*>(wbase);
+  int* bstat = reinterpret_cast<int*>(wbase + ((size_t)nsub * STRIDE * 2 + 15) / 16 * 16);
+  int* maxbin = bstat + 3 * nsub;
+
+  const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
+  const double wbd = ceil(width * (double)LSB);                      // :1603
+  if (!(wbd >= 1.0) || wbd > (double)LSB || a.lp != LSB) {
+    if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+    return;
+  }
+  const int wb = (int)wbd;
+  const int nw = LSB - wb + 1;
+  const uint8_t* sb = a.sub + c * (int64_t)nsub * LSB;
+  const int pos = lane & (SEG - 1);
+  // this lane's 16 profile bytes (a piece sits at the same offset of its band every pass)
+  uint32_t pw[4];
+  {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.prof + c * LSB + 16 * pos));
+    pw[0] = v.x;
+    pw[1] = v.y;
+    pw[2] = v.z;
+    pw[3] = v.w;
+  }
+  int P = 0, P2 = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    P = (int)__builtin_amdgcn_udot4(pw[d], 0x01010101u, (uint32_t)P, false);
+    P2 = (int)__builtin_amdgcn_udot4(pw[d], pw[d], (uint32_t)P2, false);
+  }
+  P = group_sum_i32<SEG>(P);
+  P2 = group_sum_i32<SEG>(P2);
+
+  // ---- prefix sums and the s22 sums, four 1 KiB passes per load burst ---------------------
+  const int total = nsub * LSB;
+  for (int base = 0; base < total; base += 4096) {
+    u32x4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int off = base + 1024 * u + 16 * lane;
+      q[u] = off < total ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sb + off))
+                         : (u32x4){0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int off = base + 1024 * u + 16 * lane;
+      if (base + 1024 * u >= total) break;  // wave-uniform
+      const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+      uint32_t e[16];
+      const uint32_t tot = piece_prefix(wv, e);
+      uint32_t x = tot;
+#pragma unroll
+      for (int sft = 1; sft < SEG; sft <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)x, sft);
+        if (pos >= sft) x += o;
+      }
+      const uint32_t excl = x - tot;
+      int X2 = 0, XP = 0;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        X2 = (int)__builtin_amdgcn_udot4(wv[d], wv[d], (uint32_t)X2, false);
+        XP = (int)__builtin_amdgcn_udot4(wv[d], pw[d], (uint32_t)XP, false);
+      }
+      X2 = group_sum_i32<SEG>(X2);
+      XP = group_sum_i32<SEG>(XP);
+      if (off < total) {
+        const int band = off / LSB;
+        uint16_t* row = E + band * STRIDE + 16 * pos;
+        uint32_t pk[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pk[t] = ((e[2 * t] + excl) & 0xFFFFu) | ((e[2 * t + 1] + excl) << 16);
+        reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
+        reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
+        if (pos == SEG - 1) {
+          row[16] = (uint16_t)(excl + tot);                        // E[band][LSB] = T
+          bstat[3 * band + 0] = (int)(excl + tot);
+          bstat[3 * band + 1] = X2;
+          bstat[3 * band + 2] = XP;
+        }
+      }
     }
   }
-  double var;
-  if (count > 1) {
-    var = var_med / (double)(count - 1);
-  } else {
-    double mu = 0.0;
-    for (int i = 0; i < nsub; ++i) mu += (double)maxbin[i];
-    mu /= (double)nsub;
-    var = 0.0;
-    for (int i = 0; i < nsub; ++i) var += ((double)maxbin[i] - mu) * ((double)maxbin[i] - mu);
-    var /= (double)(nsub - 1);
+  wave_lds_sync();
+
+  // ---- s22: one band per lane, then the reference's sum in band order -----------------------
+  const double inv2 = 1.0 / (double)(LSB - 1);
+  const double pvar = (double)((long long)LSB * P2 - (long long)P * P) / (double)LSB;
+  double integ = 0.0;
+  for (int i0 = 0; i0 < nsub; i0 += 64) {
+    double v = 0.0;
+    const int i = i0 + lane;
+    if (i < nsub) {
+      const int T = bstat[3 * i], X2 = bstat[3 * i + 1], XP = bstat[3 * i + 2];
+      const double d = (double)((long long)LSB * XP - (long long)T * P) / (double)LSB;
+      const double q2 = (double)((long long)LSB * X2 - (long long)T * T) / (double)LSB;
+      const double cc = fabs(sb_corr(d * inv2, q2 * inv2, pvar * inv2));
+      v = cc > 0.0055 ? cc : 0.0;  // adding 0.0 leaves the running sum's bits unchanged
+    }
+    const int cnt = nsub - i0 < 64 ? nsub - i0 : 64;
+    for (int t = 0; t < cnt; ++t) integ += bcast(v, t);
   }
-  const double rms = sqrt(var) / (double)wb;
+
+  // ---- s20 / s21 over blocks of 16 bands --------------------------------------------------
+  const double dnw = (double)nw;
+  double W[SL];
+#pragma unroll
+  for (int k = 0; k < SL; ++k) W[k] = 0.0;
+  double C = 0.0;
+  int valid = 0;
+  for (int blk = 0; blk < nsub; blk += SB_NB) {
+    const int nb = nsub - blk < SB_NB ? nsub - blk : SB_NB;
+    int bv[SB_NB][SL];
+    int sA[SB_NB], kA[SB_NB];
+    unsigned long long qA[SB_NB];
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      int sv = 0, kmax = 0;
+      unsigned long long qv = 0;
+      // branch-free: reads clamped into this wave's rows, out-of-range windows masked to 0
+      const uint16_t* row = E + (blk + ii < nsub ? blk + ii : nsub - 1) * STRIDE;
+#pragma unroll
+      for (int k = 0; k < SL; ++k) {
+        const int j = lane + 64 * k;
+        const bool in = ii < nb && j < nw;
+        const int hi = j + wb < LSB ? j + wb : LSB;
+        int b = (int)row[hi] - (int)row[j < LSB ? j : LSB];
+        b = in ? b : 0;
+        const int kk = in ? ((b << 10) | (1023 - j)) : 0;
+        kmax = kk > kmax ? kk : kmax;
+        bv[ii][k] = b;
+        sv += b;
+        qv += __umul24((uint32_t)b, (uint32_t)b);  // b < 2^16: the 24-bit multiply is exact
+      }
+      sA[ii] = sv;
+      qA[ii] = qv;
+      kA[ii] = kmax;
+    }
+    reduce_scatter16(sA, lane, [](int x, int y) { return x + y; });
+    reduce_scatter16(qA, lane, [](unsigned long long x, unsigned long long y) { return x + y; });
+    reduce_scatter16(kA, lane, [](int x, int y) { return x > y ? x : y; });
+    // lane l (< 16) now holds band bitrev4(l) of the block
+    const int beta = bitrev4(lane & 15);
+    const bool inb = beta < nb;
+    const long long N = (long long)nw * (long long)qA[0] - (long long)sA[0] * sA[0];
+    const bool ok = inb && N > 0;
+    const double rl = ok ? 1.0 / sqrt(dnw * (double)N) : 0.0;
+    const double cl = (double)sA[0] * rl;
+    if (lane < 16 && inb) maxbin[blk + beta] = 1023 - (kA[0] & 1023) + wb / 2;  // :1628
+    valid += __builtin_popcountll(__ballot(lane < 16 && ok));
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ++ii) {
+      const double r = bcast(rl, bitrev4(ii));
+      C += bcast(cl, bitrev4(ii));
+#pragma unroll
+      for (int k = 0; k < SL; ++k) W[k] = __builtin_fma(r, (double)bv[ii][k], W[k]);
+    }
+  }
+  // s21: sum_{i<k} cc_ik = (sum_j Z_j^2 - v) / 2 with Z_j = nw W_j - C, |z_i|^2 = 1
+  double zs = 0.0;
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    const double z = (lane + 64 * k < nw) ? dnw * W[k] - C : 0.0;
+    zs += z * z;
+  }
+  zs = wsum(zs);
+  const long long m = (long long)valid * (valid - 1) / 2;
+  if (m == 0) {  // ZeroDivisionError (:1681)
+    if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+    return;
+  }
+  const double mean_corr = (0.5 * (zs - (double)valid)) / (double)m;
+  wave_lds_sync();
+  const double rms = rms_of_maxbins(maxbin, nsub, wb);
   if (lane == 0) {
     double* o = a.out + c * a.ldo;
     o[0] = rms;
@@ -390,10 +654,40 @@ static hipError_t launch_sl(const SubArgs& s, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int LSB>
+static hipError_t launch_fast(const SubArgs& s, hipStream_t st) {
+  const size_t wave = fast_wave_lds<LSB>(s.nsub);
+  if (wave * 4 <= 40 * 1024) {
+    hipLaunchKernelGGL((k_subband_fast<LSB, 4>), dim3((unsigned)((s.n + 3) / 4)), dim3(256),
+                       wave * 4, st, s);
+  } else {
+    static size_t configured = 0;
+    if (wave > 48 * 1024 && wave > configured) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_subband_fast<LSB, 1>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave);
+      if (e != hipSuccess) return e;
+      configured = wave;
+    }
+    hipLaunchKernelGGL((k_subband_fast<LSB, 1>), dim3((unsigned)s.n), dim3(64), wave, st, s);
+  }
+  return hipGetLastError();
+}
+
 static hipError_t launch_sub(const SubArgs& s, hipStream_t st) {
   if (s.n <= 0) return hipSuccess;
   if (subband_shape_error(s.nsub, s.lsb)) return hipErrorInvalidValue;
   const int L = s.lsb;
+  const bool aligned = (((uintptr_t)s.sub | (uintptr_t)s.prof) & 15) == 0;
+  if (aligned && s.lp == L) {
+    switch (L) {
+      case 16: return launch_fast<16>(s, st);
+      case 32: return launch_fast<32>(s, st);
+      case 64: return launch_fast<64>(s, st);
+      case 128: return launch_fast<128>(s, st);
+      case 256: return launch_fast<256>(s, st);
+      default: break;
+    }
+  }
   if (L <= 64) return launch_sl<1, uint16_t>(s, st);
   if (L <= 128) return launch_sl<2, uint16_t>(s, st);
   if (L <= 256) return launch_sl<4, uint16_t>(s, st);

@@ -5,9 +5,10 @@ Bar (SURVEY.md §8(a) parity classes):
   * s3 (integer peak count), s4, s12-s16, s20, s22: bit-exact on every candidate;
   * every other score j (the class-X fits s1, s2, s19, s21 included) but s10/s11, row by
     row against the golden sets: on every candidate whose
-    reference score is stable -- it moves by at most STABLE relative under each of three
-    1-ulp-scale nudges of every leastsq start point (tests/golden/chaos_rows.npz,
-    tools/chaos_rows.py) -- the GPU is within 1e-5 of the reference; on the candidates
+    reference score is stable -- it moves by at most STABLE = 1e-7 relative under each of
+    seven ulp-scale perturbations of the fits (start points +-1, +-2, +4 ulp; two patterns
+    of +-1 ulp on the residuals: tests/golden/chaos_rows.npz, tools/chaos_rows.py) -- the
+    GPU is within 1e-5 of the reference; on the candidates
     where the reference itself moves, the GPU may differ, and the fraction of candidates
     differing by more than 1e-5 (1e-3) is held to 1.5 x the reference's own floor (the
     fraction of candidates moving under the nudges, tests/golden/chaos_floor.json and
@@ -31,7 +32,8 @@ from pulsarfeatureextractor_amd.synth import bates_batch
 pytestmark = pytest.mark.gpu
 
 BITEXACT = (2, 3, 11, 12, 13, 14, 15, 19, 21)
-STABLE = 1e-6                     # a reference score moving by <= this under the nudges is stable
+STABLE = 1e-7  # a reference score that moves by at most this under every nudge is stable: its
+               # value is reproducible to 7 digits, so the GPU is held to 1e-5 there
 FLOOR = json.load(open(os.path.join(GOLDEN, "chaos_floor.json")))
 ROWS = np.load(os.path.join(GOLDEN, "chaos_rows.npz"))
 

@@ -6,8 +6,9 @@ when every scipy.optimize.leastsq start point is nudged by one ulp.  This tool r
 WHICH candidates move: each golden Bates set is re-scored by the oracle (bit-exact to the
 reference on these inputs, tests/test_oracle_golden.py) under several perturbations of
 the start points -- +-1, +-2 and +4 ulp of every non-zero entry (SURVEY.md
-Appendix B: zero entries stay zero) -- and the largest relative change of every score
-over the perturbations is stored per candidate:
+Appendix B: zero entries stay zero) -- and of the residuals (two fixed patterns of
++-1 ulp on the residual vector the solver sees), and the largest relative change of every
+score over the perturbations is stored per candidate:
 
     tests/golden/chaos_rows.npz   <set>_rmax  (n, 22) float64
                                   (inf where a perturbation changes whether the candidate
@@ -44,6 +45,20 @@ def nudger(orig, steps):
     return nudged
 
 
+def residual_noise(orig, seed):
+    """Every residual vector the solver evaluates multiplied element-wise by 1 + u_i 2^-53,
+    u_i in {-1, 0, 1} from a fixed pattern: last-bit differences in the function values, the
+    kind a different evaluation or summation order produces."""
+    def nudged(f, x0, args=(), **kw):
+        def g(x, *a):
+            r = np.asarray(f(x, *a), dtype=float)
+            u = np.random.default_rng(seed + r.size).integers(-1, 2, size=r.shape)
+            return r * (1.0 + u * 2.0 ** -53)
+        return orig(g, x0, args=args, **kw)
+
+    return nudged
+
+
 def rel(a, b):
     with np.errstate(all="ignore"):
         r = np.abs(a - b) / np.maximum(np.abs(a), 1e-300)
@@ -63,8 +78,9 @@ def main():
         oka = (sa & 0xFF) == 0
         rmax = np.zeros_like(a)
         try:
-            for steps in (1, -1, 2, -2, 4):
-                B.leastsq = nudger(orig, steps)
+            for pert in (1, -1, 2, -2, 4, "r1", "r2"):
+                B.leastsq = (nudger(orig, pert) if isinstance(pert, int)
+                             else residual_noise(orig, 7 if pert == "r1" else 11))
                 b, sb = B.bates22(prof, sub, curve, scal)
                 okb = (sb & 0xFF) == 0
                 r = rel(a, b)
