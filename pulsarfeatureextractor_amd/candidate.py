@@ -5,7 +5,7 @@ Reference classes (PulsarFeatureExtractor/src/) and what replaces them here:
   CandidateFileInterface  CandidateFileInterface.py  -> CandidateFileInterface (filterScore,
                                                         isEqual, numberOfScores, epsilon)
   PHCX / SUPERBPHCX       PHCXFile.py, SUPERBPHCXFile.py -> PHCXFile / SUPERBPHCXFile
-  PFD                     PFDFile.py                 -> not in this build
+  PFD                     PFDFile.py                 -> PFDFile (pfe_pfd_dmprof, pfe_pfd_bates22)
 
 Score values come from the gfx950 kernels through the C-ABI (a batch of one candidate
 here; pulsarfeatureextractor_amd.processor batches whole directories).  As in the reference,
@@ -270,7 +270,8 @@ class Candidate:
         return self.scores
 
     def getDMCurveData(self, verbose):
-        if ".gz" not in self.candidateName or ".pfd" in self.candidateName:
+        """Candidate.py:231-255: PFD and gzipped PHCX files; [] for SUPERB PHCX."""
+        if ".pfd" not in self.candidateName and ".gz" not in self.candidateName:
             return []
         self.scores = self._file(verbose).getDMCurveData()
         return self.scores

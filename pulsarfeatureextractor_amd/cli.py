@@ -4,8 +4,8 @@
          [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K]
 
 Same flags, same output-file probing (:147-160), same mode dispatch (:215-290), for PHCX,
-SUPERB and PFD files in every mode.  --label (interactive labelling) is recognised and refused
-with exit status 2.
+SUPERB and PFD files in every mode, --label included (its prompt is commented out in the
+reference, DataProcessor.py:754-774: every candidate is labelled "0").
 """
 from __future__ import annotations
 
@@ -31,9 +31,6 @@ def main(argv=None):
     p.add_option("--device", action="store", dest="device", type="int", default=0)
     p.add_option("--workers", action="store", dest="workers", type="int", default=None)
     args, _ = p.parse_args(argv)
-    if args.label:
-        print("--label (interactive labelling) is not supported by this build.", file=sys.stderr)
-        return 2
     # output-file probing (:147-160)
     single_file = os.path.exists(args.outputPath)
     if not single_file:
@@ -56,7 +53,12 @@ def main(argv=None):
     dp = processor.DataProcessor(args.verbose, workers=args.workers)
     phcx, pfd, superb = args.phcx, args.pfd, args.superb
     try:
-        if args.dmprof:
+        if args.label:  # :220-225 (labelPFD with the two arguments ScoreGenerator passes)
+            if phcx and not pfd and not superb:
+                dp.labelPHCX(search, args.verbose)
+            elif not phcx and pfd:
+                dp.labelPFD(search, args.verbose)
+        elif args.dmprof:
             if phcx and not pfd and not superb:
                 dp.dmprofPHCX(search, args.verbose, args.outputPath, args.arff, single)
             elif not phcx and pfd and not superb:

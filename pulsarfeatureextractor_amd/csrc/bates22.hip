@@ -65,12 +65,17 @@ static size_t hand_bytes(int64_t n, int region) {
   return (size_t)hand_waves(n, region) * GLM_FPW * k * 16 * sizeof(double);
 }
 
-// workspace layout: [GaussWS x n][counters][hand-over regions][per-wave scratch]
+// waves of k_ghist_wide (each with a WIDE_SLAB_BYTES scratch slab)
+static int wide_waves(int64_t n) { return (int)(n < 256 ? (n > 0 ? n : 1) : 256); }
+
+// workspace layout: [GaussWS x n][counters][hand-over regions][wide queue][wide slabs]
+// [per-wave scratch]
 size_t bates22_workspace_bytes(const pfe_bates_in* in) {
   size_t hb = 0;
   for (int r = 0; r < 3; ++r) hb += align256(hand_bytes(in->n, r));
   return 256 + align256((size_t)in->n * sizeof(GaussWS)) +
          align256(BATES_NCOUNTERS * sizeof(unsigned)) + hb +
+         align256((size_t)in->n * sizeof(int)) + (size_t)wide_waves(in->n) * WIDE_SLAB_BYTES +
          (size_t)persistent_waves(in->n) * gdg_wave_scratch_doubles(in->lp) * sizeof(double);
 }
 
@@ -97,6 +102,11 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work, const Options& o) 
     a.hand[r] = ho ? (double*)wb : nullptr;
     wb += align256(hand_bytes(n, r));
   }
+  a.wide_list = (int*)wb;
+  wb += align256((size_t)n * sizeof(int));
+  a.wide_scr = (double*)wb;
+  a.wide_waves = wide_waves(n);
+  wb += (size_t)a.wide_waves * WIDE_SLAB_BYTES;
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());

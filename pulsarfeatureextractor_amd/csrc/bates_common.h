@@ -20,6 +20,10 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 // internal status bits (not exported)
 constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
 constexpr uint32_t ST_DEFER_HIST64 = 0x20000u;  // > 64 bins: the pooled histogram kernels pass it on
+constexpr uint32_t ST_DEFER_WIDE = 0x40000u;    // > 1024 bins: queued for k_ghist_wide
+// widest Freedman-Diaconis histogram scored (k_ghist_wide; rows in global scratch): the
+// uint8 profiles of <= 256 bins need at most ~10k (range 510 over an IQR of 1/4)
+constexpr int WIDE_MAX_BINS = 16384;
 
 // per-candidate workspace passed between the Gaussian-group kernels
 struct GaussWS {
@@ -58,6 +62,9 @@ struct BatesArgs {
   int cus;             // compute units of the device
   double* hand[3];     // hand-over scratch of the pooled kernels per stream (HAND_*), or null
   int solver;          // PFE_SOLVER_* (handle option PFE_OPT_SOLVER)
+  int* wide_list;      // candidates queued for k_ghist_wide (n entries)
+  double* wide_scr;    // per-wave row scratch of k_ghist_wide (wide_waves slabs)
+  int wide_waves;
 };
 
 constexpr int BATES_NCOUNTERS = 16;
@@ -81,7 +88,9 @@ constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernel
 static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
 // work queues of the pooled kernels (BatesArgs::counters)
 constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6,
-              CTR_GHISTG = 7, CTR_GFIXG = 8;
+              CTR_GHISTG = 7, CTR_GFIXG = 8, CTR_WIDE = 9, CTR_WIDEQ = 10;
+// one k_ghist_wide wave's scratch: the rows of a 3-parameter solve (5 arrays) + the counts
+constexpr size_t WIDE_SLAB_BYTES = (size_t)WIDE_MAX_BINS * (5 * sizeof(double) + sizeof(int));
 
 // rows per lane (MPL) the kernels use for a profile of lp bins
 __host__ __device__ constexpr int profile_mpl(int lp) {

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "lm_batch.h"
+#include "lm_global.h"
 #include "lm_group.h"
 #include "np_sum.h"
 
@@ -522,7 +523,16 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
   const int hb = g.hb, db = g.db;
   uint32_t st = 0;
   if (hb <= 0 || db <= 0) st = PFE_ST_GAUSS_FAIL;                  // histogram(bins=0) raises
-  if (!st && (hb > 64 * H || db > 64 * H)) st = BIG ? PFE_ST_UNSUPPORTED : ST_DEFER_HIST;
+  if (!st && (hb > 64 * H || db > 64 * H)) {
+    if (!BIG)
+      st = ST_DEFER_HIST;
+    else if (hb > WIDE_MAX_BINS || db > WIDE_MAX_BINS)
+      st = PFE_ST_UNSUPPORTED;
+    else {  // queue for k_ghist_wide (rows in global scratch)
+      st = ST_DEFER_WIDE;
+      if (lane == 0) a.wide_list[atomicAdd(a.counters + CTR_WIDE, 1u)] = (int)c;
+    }
+  }
   if (BIG && lane == 0) atomicAnd(&a.status[c], ~(uint32_t)(ST_DEFER_HIST));
   if (st) {
     if (lane == 0) atomicOr(&a.status[c], (uint32_t)(st));
@@ -579,6 +589,232 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     w->p_mu = fp.mu;
     w->minbg = py_min(fp.mu, ms.mean);     // :724
     w->pstd = ms.std;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Histograms wider than 1024 bins (k_ghist_wide): the profile histogram of a near-flat
+// quantised profile has thousands of Freedman-Diaconis bins (an IQR of 1/4 over a range of
+// 255).  Same fits as k_ghist, with the m rows of each solve in per-wave global scratch
+// (lm_global.h) and the counts in global memory; the bin edges are recomputed from the
+// HistSpec on every evaluation.  Candidates arrive through a queue filled by k_ghist<BIG>.
+// ---------------------------------------------------------------------------------------
+struct WideHist {  // counts of nb bins (rows >= nb are the zero padding up to m)
+  const int* cnt;
+  HistSpec h;
+  int nb, m;
+  __device__ __forceinline__ double x(int i) const { return i < nb ? h.edge(i) : 0.0; }
+  __device__ __forceinline__ double y(int i) const { return i < nb ? (double)cnt[i] : 0.0; }
+};
+
+struct GaussFnWide {  // y - |A| exp(-((x-mu)/sigma)^2 / 2) over the rows of a WideHist
+  WideHist w;
+  int nsl;
+  template <class D>
+  __device__ __forceinline__ double model(const D& dv, const double (&p)[3], double xv) const {
+    const double t = dv(xv - p[1]);
+    return fabs(p[2]) * exp(-(t * t) / 2.0);
+  }
+  __device__ __forceinline__ void operator()(const double (&p)[3], double* f) const {
+    const int lane = lane_id();
+    with_div(p[0], p[1], [&](const auto& dv) {
+      for (int k = 0; k < nsl; ++k) {
+        const int i = lane + 64 * k;
+        f[k * 64 + lane] = i < w.m ? w.y(i) - model(dv, p, w.x(i)) : 0.0;
+      }
+    });
+  }
+};
+
+struct GaussFixedFnWide {  // mu fixed at xmax; parameters (sigma, A)
+  WideHist w;
+  int nsl;
+  double xmax;
+  __device__ __forceinline__ void operator()(const double (&p)[2], double* f) const {
+    const int lane = lane_id();
+    with_div(p[0], xmax, [&](const auto& dv) {
+      for (int k = 0; k < nsl; ++k) {
+        const int i = lane + 64 * k;
+        double v = 0.0;
+        if (i < w.m) {
+          const double t = dv(w.x(i) - xmax);
+          v = w.y(i) - fabs(p[1]) * exp(-(t * t) / 2.0);
+        }
+        f[k * 64 + lane] = v;
+      }
+    });
+  }
+};
+
+// fitGaussian (:774-983) on a wide histogram: fit_gaussian_hist with the rows in memory
+__device__ HistFit fit_gaussian_hist_wide(const WideHist& w, double* scr, int lane) {
+  HistFit r{0, 0, 0, false};
+  const int nb = w.nb;
+  const int nsl = (w.m + 63) / 64;
+  double cmax = -1.0, s = 0.0;
+  int imax = 1 << 30;
+  for (int k = 0; k < nsl; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nb) {
+      const double v = w.y(i);
+      s += v;
+      if (v > cmax) {
+        cmax = v;
+        imax = i;
+      }
+    }
+  }
+  const ArgMax am = wargmax(cmax, imax);
+  const int idx = am.i;
+  const double a0 = am.v;
+  const double mean = wsum(s) / (double)nb;
+  double q = 0.0;
+  for (int k = 0; k < nsl; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nb) {
+      const double d = w.y(i) - mean;
+      q += d * d;
+    }
+  }
+  const double s0 = sqrt(wsum(q) / (double)nb);
+  const double meansq = mean * mean;
+  GaussFnWide fn{w, nsl};
+  const RowStore<3> rs{scr, nsl};
+  double mu0 = w.x(idx);
+  int retry = 0;
+  double p[3];
+  for (;;) {
+    p[0] = s0;
+    p[1] = mu0;
+    p[2] = a0;
+    lmdif_g<3>(fn, p, 200 * 4, rs);
+    double cs = 0.0;
+    for (int k = 0; k < nsl; ++k) {
+      const int i = lane + 64 * k;
+      if (i < nb) {
+        const double d = w.y(i) - fn.model(PlainDiv{p[0]}, p, w.x(i));
+        cs += d * d;
+      }
+    }
+    const double chisq = wsum(cs) / (double)w.m;
+    if ((chisq > meansq * (double)nb) && (p[0] < 0.2 * (double)nb)) {
+      ++retry;
+      if (idx + retry > nb) {  // numpy.delete index out of bounds
+        r.fail = true;
+        return r;
+      }
+      double bv = -1.0;
+      int bi = 1 << 30;
+      for (int k = 0; k < nsl; ++k) {
+        const int i = lane + 64 * k;
+        if (i < nb && (i < idx || i >= idx + retry) && w.y(i) > bv) {
+          bv = w.y(i);
+          bi = i;
+        }
+      }
+      const ArgMax t = wargmax(bv, bi);
+      if (t.i >= (1 << 30)) {
+        r.fail = true;
+        return r;
+      }
+      const int pos = t.i < idx ? t.i : t.i - retry;
+      if (pos + retry >= w.m) {
+        r.fail = true;
+        return r;
+      }
+      mu0 = w.x(pos + retry);
+      if (retry > 5) break;
+    } else {
+      break;
+    }
+  }
+  r.sigma = p[0];
+  r.mu = p[1];
+  r.amp = p[2];
+  return r;
+}
+
+// numpy.histogram counts of val[ok] into global cnt[0, nb)
+template <int P, class V>
+__device__ __forceinline__ void build_hist_wide(int* cnt, const HistSpec& h, const V (&val)[P],
+                                                const bool (&ok)[P]) {
+  const int lane = lane_id();
+  for (int i = lane; i < h.nb; i += 64) cnt[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (ok[k]) atomicAdd(&cnt[hist_bin(h, val[k])], 1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int P, bool F>
+__global__ __launch_bounds__(64) void k_ghist_wide(BatesArgs a) {
+  __shared__ double stage[F ? 64 * P : 1];
+  const int lane = lane_id();
+  const unsigned total = a.counters[CTR_WIDE];
+  char* slab = (char*)a.wide_scr + (size_t)blockIdx.x * WIDE_SLAB_BYTES;
+  double* scr = (double*)slab;
+  int* cnt = (int*)(slab + (size_t)WIDE_MAX_BINS * 5 * sizeof(double));
+  for (;;) {
+    const int64_t q = queue_next(a.counters + CTR_WIDEQ);
+    if (q >= (int64_t)total) break;
+    const int64_t c = a.wide_list[q];
+    GhPre<P, F> g;
+    ghist_prologue<P, F>(a, c, g);
+    const int hb = g.hb, db = g.db;
+    // ---- derivative histogram and its fit (:657-661)
+    const HistSpec hd = hist_spec(g.dmin, g.dmax, db);
+    build_hist_wide<P>(cnt, hd, g.d, g.okd);
+    const HistFit fd = fit_gaussian_hist_wide(WideHist{cnt, hd, db, db < 3 ? 3 : db}, scr, lane);
+    // ---- profile histogram and its fits (:678-705)
+    const HistSpec hp = hist_spec(g.vmin, g.vmax, hb);
+    build_hist_wide<P>(cnt, hp, g.v, g.okv);
+    const WideHist wp{cnt, hp, hb, hb < 3 ? 3 : hb};
+    const HistFit fp = fit_gaussian_hist_wide(wp, scr, lane);
+    uint32_t st = 0;
+    if (fd.fail || fp.fail || hb < 2) st = PFE_ST_GAUSS_FAIL;
+    if (!st) {
+      // fixed-mean fit (:1034-1045): xmax = xData[int(bins/2)-1]
+      int xi = hb / 2 - 1;
+      if (xi < 0) xi += hb;
+      const int nsl = (hb + 63) / 64;
+      GaussFixedFnWide fx{WideHist{cnt, hp, hb, hb}, nsl, hp.edge(xi)};
+      double cmax = -1.0, s = 0.0;
+      for (int k = 0; k < nsl; ++k) {
+        const int i = lane + 64 * k;
+        if (i < hb) {
+          cmax = fmax(cmax, fx.w.y(i));
+          s += fx.w.y(i);
+        }
+      }
+      cmax = wmax(cmax);
+      const double mean = wsum(s) / (double)hb;
+      double qq = 0.0;
+      for (int k = 0; k < nsl; ++k) {
+        const int i = lane + 64 * k;
+        if (i < hb) qq += (fx.w.y(i) - mean) * (fx.w.y(i) - mean);
+      }
+      double pf[2] = {sqrt(wsum(qq) / (double)hb), cmax};
+      lmdif_g<2>(fx, pf, 200 * 3, RowStore<2>{scr, nsl});
+      const MeanStd ms = ghist_meanstd<P, F>(g, a.lp, stage);
+      if (lane == 0) {
+        double* o = a.out + c * 22;
+        o[4] = fabs(fx.xmax - fp.mu);          // s5 (:715)
+        o[5] = fabs(pf[1] / fp.amp);           // s6 (:716)
+        o[6] = fabs(fd.mu - fp.mu);            // s7 (:717)
+        GaussWS* w = a.ws + c;
+        w->p_mu = fp.mu;
+        w->minbg = py_min(fp.mu, ms.mean);     // :724
+        w->pstd = ms.std;
+      }
+    }
+    if (lane == 0) {
+      if (st) atomicOr(&a.status[c], st);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      atomicAnd(&a.status[c], ~ST_DEFER_WIDE);
+    }
   }
 }
 
@@ -2048,6 +2284,11 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((k_ghist<P, 4, false, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
       hipLaunchKernelGGL((k_ghist<P, 16, true, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
     }                                                                                   \
+    /* > 1024 bins: the queue k_ghist<BIG> filled */                                    \
+    if (a.fprof)                                                                        \
+      hipLaunchKernelGGL((k_ghist_wide<P, true>), dim3((unsigned)a.wide_waves), dim3(64), 0, st, a); \
+    else                                                                                \
+      hipLaunchKernelGGL((k_ghist_wide<P, false>), dim3((unsigned)a.wide_waves), dim3(64), 0, st, a); \
     if (use_glm)                                                                        \
       hipLaunchKernelGGL((k_gt1g<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                        \
     else if (use_blm)                                                                   \

@@ -9,16 +9,22 @@ packed into dense arrays and scored in large batches on the GPU through libpfe.
   processPHCXCollectively / processSUPERBCollectively  (:109-146, :451-599)
   processPHCXSeparately                                (:91-105, :603-687)
   dmprofPHCX / dmprofSUPERB                            (:255-301, :830-994)
+  label                                                (:691-826)
 PFD files (".pfd" in the name, Candidate.py:136) are read by pfd.read and go through
-pfe_pfd_dmprof (dmprof and profile-bin modes); the PFD 22-score path is not in this build
-yet and raises.  --label is interactive and out of scope.
+pfe_pfd_dmprof (dmprof, profile-bin and label modes) and pfe_pfd_bates22 (22 scores).
+
+Streaming: the paths are taken in batches of BATCH files; batch k+1 is parsed on the host
+(native reader threads; the ctypes call releases the GIL) while batch k is scored on the
+GPU, and each batch's output lines are appended as soon as it is scored -- memory is bounded
+by the batch, not the directory.  The reference buffers every line and appends once at the
+end (DataProcessor.py:590-594); the final file content is the same, in discovery order.
 """
 from __future__ import annotations
 
 import datetime
 import fnmatch
 import os
-from concurrent.futures import ProcessPoolExecutor
+from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 
 import numpy as np
 
@@ -26,6 +32,8 @@ from . import pfd as _pfd
 from . import phcx as _phcx
 from . import writers
 from .candidate import get_engine, status_error
+
+BATCH = 8192  # files per streamed batch
 
 PHCX_RE = "*.phcx.gz"
 SUPERB_RE = "*.phcx"
@@ -149,6 +157,28 @@ def score_pfd22(datas, engine=None, batch: int = 1 << 16):
     return out, err
 
 
+def pfd_profile_and_curve(datas, engine=None, batch: int = 1 << 14):
+    """The 0..255 profile and the float32 chi^2-vs-DM curve of parsed PFD folds
+    (PFDFile.computeProfileScores :479-492, getDMCurveData :494-520):
+    -> (profiles [n arrays], curves [n float32 arrays], error or None per fold)."""
+    engine = engine or get_engine()
+    n = len(datas)
+    profiles, curves, err = [None] * n, [None] * n, [None] * n
+    groups: dict = {}
+    for i, d in enumerate(datas):
+        groups.setdefault((d.npart, d.nsub, d.proflen), []).append(i)
+    for _shape, idx in groups.items():
+        for s0 in range(0, len(idx), batch):
+            part = idx[s0:s0 + batch]
+            r = engine.pfd_dmprof(*_pfd.batch_inputs([datas[i] for i in part]), lyon8=False)
+            for j, i in enumerate(part):
+                profiles[i] = r["profile"][j]
+                curves[i] = r["chis"][j]
+                if int(r["status"][j]) & 0x20:
+                    err[i] = "Exception: DM curve extraction exception"
+    return profiles, curves, err
+
+
 def _shape_key(c):
     return (len(c.profile), c.subbands.shape[0], c.subbands.shape[1], len(c.dm_curve))
 
@@ -198,19 +228,37 @@ def score_lyon8(cands, engine=None):
     return out
 
 
+def _stream(paths, parse, score, emit, batch=BATCH):
+    """parse(batch paths) on a helper thread one batch ahead of score(parsed) on the calling
+    thread; emit(batch offset, batch paths, results) in discovery order."""
+    if not paths:
+        return
+    cuts = list(range(0, len(paths), batch)) + [len(paths)]
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        fut = ex.submit(parse, paths[cuts[0]:cuts[1]])
+        for k in range(len(cuts) - 1):
+            parsed = fut.result()
+            if k + 2 < len(cuts):
+                fut = ex.submit(parse, paths[cuts[k + 1]:cuts[k + 2]])
+            emit(cuts[k], paths[cuts[k]:cuts[k + 1]], score(parsed))
+
+
 class DataProcessor:
     """Same entry points and output semantics as DataProcessor.py, batched on the GPU."""
 
-    def __init__(self, debugFlag=False, engine=None, workers=None, log=print):
+    def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH):
         self.debug = debugFlag
         self.engine = engine
         self.workers = workers
         self.log = log
+        self.batch = batch
         self.scoreStore = []
         self.candidateErrorLog = "CandidateErrorLog.txt"
         self.superb = False
         self.phcx = False
         self.pfd = False
+        self.positive = 0
+        self.negative = 0
         if not os.path.exists(self.candidateErrorLog):       # :86-87
             writers.append_text(self.candidateErrorLog, "")
 
@@ -229,46 +277,68 @@ class DataProcessor:
         self.log(f"Error reading profile data :\n\t{why}\n{cand}  did not have scores generated.")
         writers.append_text(self.candidateErrorLog, cand + "\n")
 
-    def _finish(self, outPath, processed, ok, failed, start):
+    def _summary(self, processed, ok, failed, start, extra=""):
         end = datetime.datetime.now()
-        writers.append_text(outPath, "".join(s + "\n" for s in self.scoreStore))
         self.log(f"\nCandidates processed:\t{processed}\nSuccesses:\t{ok}\nFailures:\t{failed}\n"
-                 f"Execution time:  {end - start}")
+                 f"{extra}Execution time:  {end - start}")
 
-    # ---- 22 scores / profile bins ---------------------------------------------------
-    def _rows(self, paths, genProfileData):
-        """{index: (row, None)} or {index: (None, error)} in discovery order: PHCX / SUPERB
-        files through the native reader and pfe_bates22, PFD files through the host reader
-        and pfe_pfd_bates22 (or the profile bins, --profile)."""
-        res = {}
+    # ---- parse / score stages ---------------------------------------------------------
+    def _parse(self, paths):
+        """Host stage: PHCX / SUPERB files through the native reader (Python parser for the
+        files it flags), PFD files through pfd.read.  -> (px, parsed, pf, read)."""
         px = [i for i, p in enumerate(paths) if not is_pfd(p)]
         pf = [i for i, p in enumerate(paths) if is_pfd(p)]
+        parsed = parse_all([paths[i] for i in px], self.workers) if px else []
+        rd = [_read_pfd(paths[i]) for i in pf]
+        return px, parsed, pf, rd
+
+    def _score(self, pre, mode):
+        """GPU stage.  mode: "scores" (22 scores), "profile" (profile bins), "lyon8" (the 8
+        Lyon features) or "label" ((scores, profile, DM-curve data)).
+        -> {batch index: (row, None) | (None, error)}"""
+        px, parsed, pf, rd = pre
+        res = {}
         if px:
-            parsed = parse_all([paths[i] for i in px], self.workers)
             good = [k for k, (c, e) in enumerate(parsed) if c is not None]
             cands = [parsed[k][0] for k in good]
-            if genProfileData:
+            errs = [None] * len(cands)
+            if mode == "profile":
                 rows = [[float(v) for v in c.profile] for c in cands]
-                errs = [None] * len(cands)
+            elif mode == "lyon8":
+                f = score_lyon8(cands, self.engine) if cands else np.zeros((0, 8))
+                rows = [f[j] for j in range(len(cands))]
             else:
                 sc, errs = score_bates(cands, self.engine)
-                rows = [sc[j] for j in range(len(cands))]
+                if mode == "label":  # Candidate.calculateProfileScores / getDMCurveData
+                    rows = [(sc[j], [float(v) for v in c.profile],
+                             list(c.lyon_dm) if not c.superb else [])
+                            for j, c in enumerate(cands)]
+                else:
+                    rows = [sc[j] for j in range(len(cands))]
             for j, k in enumerate(good):
                 res[px[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
             for k, (c, e) in enumerate(parsed):
                 if c is None:
                     res[px[k]] = (None, e)
         if pf:
-            rd = [_read_pfd(paths[i]) for i in pf]
             good = [k for k, (d, e) in enumerate(rd) if d is not None]
             datas = [rd[k][0] for k in good]
-            if genProfileData:       # PFDFile.computeProfileScores (:479-492)
+            if mode == "profile":       # PFDFile.computeProfileScores (:479-492)
                 _f, profiles, _e = score_pfd(datas, self.engine)
                 rows = [[float(v) for v in pr] for pr in profiles]
                 errs = [None] * len(datas)
+            elif mode == "lyon8":
+                feats, _prof, errs = score_pfd(datas, self.engine)
+                rows = [feats[j] for j in range(len(datas))]
             else:
                 sc, errs = score_pfd22(datas, self.engine)
-                rows = [sc[j] for j in range(len(datas))]
+                if mode == "label":
+                    prof, chis, derr = pfd_profile_and_curve(datas, self.engine)
+                    rows = [(sc[j], [float(v) for v in prof[j]], list(chis[j]))
+                            for j in range(len(datas))]
+                    errs = [e or de for e, de in zip(errs, derr)]
+                else:
+                    rows = [sc[j] for j in range(len(datas))]
             for j, k in enumerate(good):
                 res[pf[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
             for k, (d, e) in enumerate(rd):
@@ -276,6 +346,25 @@ class DataProcessor:
                     res[pf[k]] = (None, e)
         return res
 
+    def _run(self, paths, mode, on_row):
+        """Stream the paths through parse -> score; on_row(path, row) for every scored
+        candidate (in discovery order), the reference's failure handling for the rest."""
+        counts = {"ok": 0, "failed": 0}
+
+        def emit(_off, batch_paths, res):
+            for i, p in enumerate(batch_paths):
+                row, err = res[i]
+                if row is None:
+                    self._fail(p, err)
+                    counts["failed"] += 1
+                else:
+                    on_row(p, row)
+                    counts["ok"] += 1
+
+        _stream(paths, self._parse, lambda pre: self._score(pre, mode), emit, self.batch)
+        return counts["ok"], counts["failed"]
+
+    # ---- 22 scores / profile bins ---------------------------------------------------
     def processCollectively(self, directory, verbose, regexes, outPath, arff, genProfileData,
                             single):
         if arff:                                              # prepareARFFFile (:329-367)
@@ -287,17 +376,32 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        res = self._rows(paths, genProfileData)
-        ok = failed = 0
-        for i, p in enumerate(paths):
-            s, e = res[i]
-            if s is None:
-                self._fail(p, e)
-                failed += 1
-                continue
-            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
-            ok += 1
-        self._finish(outPath, len(paths), ok, failed, start)
+        pending = []
+
+        def on_row(p, s):
+            pending.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
+
+        def flush():
+            if pending:
+                writers.append_text(outPath, "".join(x + "\n" for x in pending))
+                pending.clear()
+
+        counts = {"ok": 0, "failed": 0}
+
+        def emit(_off, batch_paths, res):
+            for i, p in enumerate(batch_paths):
+                row, err = res[i]
+                if row is None:
+                    self._fail(p, err)
+                    counts["failed"] += 1
+                else:
+                    on_row(p, row)
+                    counts["ok"] += 1
+            flush()  # append this batch's lines now (bounded memory, partial output survives)
+
+        mode = "profile" if genProfileData else "scores"
+        _stream(paths, self._parse, lambda pre: self._score(pre, mode), emit, self.batch)
+        self._summary(len(paths), counts["ok"], counts["failed"], start)
 
     def processPFDCollectively(self, directory, verbose, outPath, arff, genProfileData,
                                processSingleCandidate):
@@ -319,15 +423,15 @@ class DataProcessor:
 
     def processSeparately(self, directory, verbose, regexes, single):
         """:603-687 — each candidate's 22 scores into <candidate>.dat."""
+        start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        res = self._rows(paths, False)
-        for i, p in enumerate(paths):
-            s, e = res[i]
-            if s is None:
-                self._fail(p, e)
-            else:
-                with open(p + ".dat", "w") as f:                   # outputScores :429-447
-                    f.write(writers.dat_text(s))
+
+        def on_row(p, s):
+            with open(p + ".dat", "w") as f:                   # outputScores :429-447
+                f.write(writers.dat_text(s))
+
+        ok, failed = self._run(paths, "scores", on_row)
+        self._summary(len(paths), ok, failed, start)
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
         self.phcx = True
@@ -339,46 +443,24 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        row, why = self._lyon_rows(paths)
-        ok = failed = 0
-        for i, p in enumerate(paths):
-            if i not in row:
-                self._fail(p, why.get(i))
-                failed += 1
-                continue
-            s = row[i]
-            self.scoreStore.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
-            ok += 1
-        self._finish(outPath, len(paths), ok, failed, start)
+        pending = []
+        counts = {"ok": 0, "failed": 0}
 
-    def _lyon_rows(self, paths):
-        """{index: 8 features} for the files that score, {index: error} for the rest; PHCX /
-        SUPERB files through pfe_lyon8_u8, PFD files through pfe_pfd_dmprof."""
-        row, why = {}, {}
-        px = [i for i, p in enumerate(paths) if not is_pfd(p)]
-        pf = [i for i, p in enumerate(paths) if is_pfd(p)]
-        if px:
-            parsed = parse_all([paths[i] for i in px], self.workers)
-            good = [k for k, (c, e) in enumerate(parsed) if c is not None]
-            feats = score_lyon8([parsed[k][0] for k in good], self.engine)
-            for j, k in enumerate(good):
-                row[px[k]] = feats[j]
-            for k, (c, e) in enumerate(parsed):
-                if c is None:
-                    why[px[k]] = e
-        if pf:
-            rd = [_read_pfd(paths[i]) for i in pf]
-            good = [k for k, (d, e) in enumerate(rd) if d is not None]
-            feats, _prof, errs = score_pfd([rd[k][0] for k in good], self.engine)
-            for j, k in enumerate(good):
-                if errs[j]:
-                    why[pf[k]] = errs[j]
-                else:
-                    row[pf[k]] = feats[j]
-            for k, (d, e) in enumerate(rd):
-                if d is None:
-                    why[pf[k]] = e
-        return row, why
+        def emit(_off, batch_paths, res):
+            for i, p in enumerate(batch_paths):
+                row, err = res[i]
+                if row is None:
+                    self._fail(p, err)
+                    counts["failed"] += 1
+                    continue
+                pending.append(writers.arff_line(p, row) if arff else writers.score_line(p, row))
+                counts["ok"] += 1
+            if pending:
+                writers.append_text(outPath, "".join(x + "\n" for x in pending))
+                pending.clear()
+
+        _stream(paths, self._parse, lambda pre: self._score(pre, "lyon8"), emit, self.batch)
+        self._summary(len(paths), counts["ok"], counts["failed"], start)
 
     def dmprofPFD(self, directory, verbose, outPath, arff, processSingleCandidate):
         self.pfd = True
@@ -407,9 +489,59 @@ class DataProcessor:
         self.processCollectively(directory, verbose, [PHCX_RE] + list(PFD_RES), outPath, arff,
                                  genProfileData, processSingleCandidate)
 
-    # ---- not in this build -------------------------------------------------------------
-    def _label(self, *a, **k):
-        raise NotImplementedError("--label (interactive labelling, DataProcessor.py:691-826) "
-                                  "is not in this build")
+    # ---- label mode (:691-826) --------------------------------------------------------
+    def label(self, directory, verbose, regexes):
+        """Scores.csv, Profile.csv, DMCurve.csv and Cands.meta in the candidate directory:
+        per candidate the 22 scores, the profile bins and the DM-curve data, each row ending
+        in the label and ",%<candidate>".  The reference's interactive prompt is commented
+        out (:754-774), so every label is "0" and the positive/negative counts stay 0.
+        Values are written as the reference's Python-2 str() writes them (no nan/inf
+        replacement here, unlike storeScore)."""
+        if directory == "":
+            directory = os.path.dirname(os.path.realpath(__file__))
+        meta = directory + "/Cands.meta"
+        files = {"scores": directory + "/Scores.csv", "profile": directory + "/Profile.csv",
+                 "dm": directory + "/DMCurve.csv"}
+        start = datetime.datetime.now()
+        paths = discover(directory, regexes)
+        lab = "0"
+        out = {k: [] for k in ("scores", "profile", "dm", "meta")}
 
-    labelPHCX = labelPFD = _label
+        def on_row(p, row):
+            sc, prof, dmc = row
+            out["scores"].append("".join(writers.py2_str(v) + "," for v in sc) + lab + ",%" + p + "\n")
+            out["profile"].append("".join(writers.py2_str(v) + "," for v in prof) + lab + ",%" + p + "\n")
+            out["dm"].append("".join(writers.py2_scalar_str(v) + "," for v in dmc) + lab + ",%" + p + "\n")
+            out["meta"].append(p + "," + lab + "\n")
+
+        counts = {"ok": 0, "failed": 0}
+
+        def emit(_off, batch_paths, res):
+            for i, p in enumerate(batch_paths):
+                row, err = res[i]
+                if row is None:
+                    self._fail(p, err)
+                    counts["failed"] += 1
+                else:
+                    on_row(p, row)
+                    counts["ok"] += 1
+            for k, path in (("scores", files["scores"]), ("profile", files["profile"]),
+                            ("dm", files["dm"]), ("meta", meta)):
+                if out[k]:
+                    writers.append_text(path, "".join(out[k]))
+                    out[k].clear()
+
+        _stream(paths, self._parse, lambda pre: self._score(pre, "label"), emit, self.batch)
+        self._summary(len(paths), counts["ok"], counts["failed"], start,
+                      f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n")
+
+    def labelPHCX(self, directory, verbose):
+        self.phcx = True
+        self.label(directory, verbose, [PHCX_RE])
+
+    def labelPFD(self, directory, verbose, outPath=None, arff=None, genProfileData=None,
+                 processSingleCandidate=None):
+        """The reference declares six parameters but ScoreGenerator.py:225 passes two (a
+        TypeError); the extra ones are optional here and unused, as in the reference."""
+        self.pfd = True
+        self.label(directory, verbose, list(PFD_RES))

@@ -32,6 +32,27 @@ def py2_str(x) -> str:
     return s
 
 
+def py2_scalar_str(x) -> str:
+    """Python-2 str() of a numpy scalar as the label writer meets them: integers as
+    integers (the PHCX DM-curve data, PHCXOperations.getDM_FFT :279-293), float32 with 8
+    significant digits (old numpy's float32 str; the PFD chi^2 curve), float64 as py2_str."""
+    import numpy as np
+
+    if isinstance(x, (int, np.integer)):
+        return str(int(x))
+    if isinstance(x, np.float32):
+        v = float(x)
+        if math.isnan(v):
+            return "nan"
+        if math.isinf(v):
+            return "inf" if v > 0 else "-inf"
+        s = "%.8g" % v
+        if "." not in s and "e" not in s:
+            s += ".0"
+        return s
+    return py2_str(x)
+
+
 def _clean(s: str) -> str:
     return s.replace("nan", "0").replace("inf", "0")
 

@@ -1,5 +1,6 @@
 """Load tests/golden/*.npz (made by tools/make_golden.py from the reference itself)."""
 import os
+import sys
 
 import numpy as np
 
@@ -35,35 +36,37 @@ def bates_inputs(d):
 
 
 def oracle_with_floor(prof, sub, curve, scal):
-    """Oracle scores of a fresh batch plus that batch's own chaos floor: the fraction of
-    candidates whose score moves (> 1e-5 / > 1e-3 relative) when every leastsq start point
-    is nudged by one ulp (the tools/chaos_floor.py procedure, applied to this batch)."""
+    """Oracle scores of a fresh batch plus that batch's own chaos data (tools/chaos_rows.py,
+    applied to this batch): every leastsq start point nudged by +-1, +-2 and +4 ulp, and two
+    patterns of +-1 ulp on the residuals.  Returns (scores, status, floor, rmax): floor = the
+    fraction of candidates whose score moves by > 1e-5 / > 1e-3 relative under any of them,
+    rmax (n, 22) = each candidate's largest relative move."""
     import warnings
 
     import oracle.bates as B
 
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "tools"))
+    from chaos_rows import nudger, rel, residual_noise
+
     orig = B.leastsq
-
-    def nudged(f, x0, args=(), **kw):
-        x = np.array(x0, dtype=float).copy()
-        nz = x != 0
-        x[nz] = np.nextafter(x[nz], np.inf)
-        return orig(f, x, args=args, **kw)
-
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         a, sa = B.bates22(prof, sub, curve, scal)
+        oka = (sa & 0xFF) == 0
+        rmax = np.zeros_like(a)
         try:
-            B.leastsq = nudged
-            b, sb = B.bates22(prof, sub, curve, scal)
+            for pert in (nudger(orig, 1), nudger(orig, -1), nudger(orig, 2), nudger(orig, -2),
+                         nudger(orig, 4), residual_noise(orig, 7), residual_noise(orig, 11)):
+                B.leastsq = pert
+                b, sb = B.bates22(prof, sub, curve, scal)
+                okb = (sb & 0xFF) == 0
+                r = rel(a, b)
+                r[oka != okb] = np.inf
+                r[~oka & ~okb] = 0.0
+                rmax = np.maximum(rmax, r)
         finally:
             B.leastsq = orig
-    ok = ((sa & 0xFF) == 0) & ((sb & 0xFF) == 0)
-    with np.errstate(all="ignore"):
-        r = np.abs(a - b) / np.maximum(np.abs(a), 1e-300)
-    r[(a == b) | (np.isnan(a) & np.isnan(b))] = 0.0
-    r[np.isnan(r)] = np.inf
-    r = r[ok]
+    r = rmax[oka]
     floor = {"moved_1e-5": (r > 1e-5).mean(axis=0).tolist(),
              "moved_1e-3": (r > 1e-3).mean(axis=0).tolist()}
-    return a, sa, floor
+    return a, sa, floor, rmax

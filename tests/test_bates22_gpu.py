@@ -17,7 +17,11 @@ Bar (SURVEY.md §8(a) parity classes):
     reference does not reproduce ITSELF there -- the same candidate scored twice in one
     process moves s10/s11 in 4-18% of rows (tests/test_oracle_golden.py) --
     so a golden value of a candidate that is stable under the nudges is still not a pin;
-  * fresh (non-golden) batches are checked against the oracle with that batch's own floor.
+  * fresh (non-golden) batches are checked against the oracle the same way with that
+    batch's own perturbation data, one stable candidate per score excepted: a candidate
+    stable under the seven deterministic perturbations can still change basin under
+    per-step ulp noise -- tools/basin_probe.py shows the reference itself reaching the GPU's
+    value for the one lp=200 candidate this allowance covers (profiles/).
 """
 import json
 import os
@@ -26,7 +30,6 @@ import numpy as np
 import pytest
 
 from golden_util import GOLDEN, SELF_NOISY, bates_inputs, load, oracle_with_floor
-from oracle.bates import bates22 as oracle_bates22
 from pulsarfeatureextractor_amd.synth import bates_batch
 
 pytestmark = pytest.mark.gpu
@@ -47,11 +50,15 @@ def rel_err(got, ref):
     return r
 
 
-def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(), rmax=None):
+def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(), rmax=None,
+                  stable_slack=0):
     """close: scores held to <= 1e-12 relative instead of bit-exactness -- s20/s22 at lengths
     where numpy's BLAS dot products sum in another order than a power-of-two tree (the
     difference is an ulp).  rmax: (n, 22) per-candidate reference movement under the
-    start-point nudges (golden sets): row-conditioned parity on the stable candidates."""
+    perturbations: row-conditioned parity on the stable candidates, of which stable_slack
+    per score may still differ (fresh batches: a candidate that is stable under the seven
+    deterministic perturbations can still change basin under per-step noise, see
+    tools/basin_probe.py)."""
     gok = (st & 0xFF) == 0
     assert np.array_equal(gok, ref_ok), f"{tag}: failure pattern differs"
     got, ref = out[gok], ref[gok]
@@ -70,7 +77,7 @@ def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(),
             continue
         if stable is not None and j not in SELF_NOISY:
             bad = np.where(stable[:, j] & (r[:, j] > 1e-5))[0]
-            assert len(bad) == 0, (f"{tag}: s{j + 1} beyond 1e-5 on {len(bad)} candidates where "
+            assert len(bad) <= stable_slack, (f"{tag}: s{j + 1} beyond 1e-5 on {len(bad)} candidates where "
                                    f"the reference is stable (rows {bad[:10].tolist()})")
         for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3")):
             moved = (r[:, j] > tol).mean()
@@ -79,19 +86,23 @@ def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(),
                                       f"(reference 1-ulp floor {floor[key][j]:.3f})")
 
 
-@pytest.mark.parametrize("name", ["bates22_phcx128", "bates22_superb64"])
+@pytest.mark.parametrize("name", ["bates22_phcx128", "bates22_superb64", "bates22_phcx128_wide"])
 def test_vs_reference_golden(engine, name):
     d = load(name)
     prof, sub, curve, scal = bates_inputs(d)
     out, st = engine.bates22(prof, sub, curve, scal)
-    check_against(out, st, d["out"], d["ok"], name, FLOOR[name], rmax=ROWS[f"{name}_rmax"])
+    assert not (st & 0x10).any(), "PFE_ST_UNSUPPORTED"
+    check_against(out, st, d["out"], d["ok"], name, FLOOR.get(name, FLOOR["bates22_phcx128"]),
+                  rmax=ROWS[f"{name}_rmax"])
 
 
 def test_vs_oracle_fresh_inputs(engine):
     b = bates_batch(160, seed=77)
     out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    ref, rst = oracle_bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", FLOOR["bates22_phcx128"])
+    ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    gold = FLOOR["bates22_phcx128"]
+    floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
+    check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", floor, rmax=rmax, stable_slack=1)
 
 
 @pytest.mark.parametrize("lp,n", [(256, 96), (100, 64), (200, 48), (512, 24)])
@@ -100,14 +111,14 @@ def test_vs_oracle_other_lengths(engine, lp, n):
     kernels (lp > 256: 16 rows per lane, wide histograms)."""
     b = bates_batch(n, lp=lp, lsb=lp, seed=1000 + lp)
     out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    ref, rst, own = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     pow2 = lp & (lp - 1) == 0
     exact = BITEXACT if pow2 else tuple(j for j in BITEXACT if j not in (19, 21))
     # floor: the larger of this batch's own 1-ulp floor and the 128-bin golden floor
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
     check_against(out, st, ref, (rst & 0xFF) == 0, f"oracle lp={lp}", floor,
-                  bitexact=exact, close=() if pow2 else (19, 21))
+                  bitexact=exact, close=() if pow2 else (19, 21), rmax=rmax, stable_slack=1)
 
 
 def test_batched_solver_bit_identical(engine):
@@ -189,16 +200,17 @@ def test_pooled_group_solver(engine, lp):
 
 def wide_histogram_batch(n, seed):
     """Profiles with low noise under a strong narrow pulse: Freedman-Diaconis bin counts of
-    ~40 (pooled kernels), ~100-190 (deferred to the wave kernel, > 64 bins) and ~350-390
-    (the wide-histogram kernel, > 256 bins)."""
+    ~40 (pooled kernels), ~100-190 (deferred to the wave kernel, > 64 bins), ~350-390
+    (the 1024-bin wave kernel, > 256 bins) and, from quantised sigma ~ 0.5 noise, often
+    1000-1600 (k_ghist_wide, rows in global scratch)."""
     b = bates_batch(n, seed=seed)
     rng = np.random.default_rng(seed)
     lp = b["prof"].shape[1]
     x = np.arange(lp)
     prof = np.empty((n, lp))
     for i in range(n):
-        kind = i % 3
-        sd = (2.5, 0.7, 6.0)[kind]
+        kind = i % 4
+        sd = (2.5, 0.7, 6.0, 0.5)[kind]
         base = rng.normal(100 if kind != 1 else 50, sd, lp)
         mu, w = rng.uniform(10, lp - 10), rng.uniform(1.0, 3.0)
         prof[i] = base + 150 * np.exp(-0.5 * ((x - mu) / w) ** 2)
@@ -208,14 +220,22 @@ def wide_histogram_batch(n, seed):
 
 def test_wide_histograms_vs_oracle(engine):
     """Every histogram-width class in one batch: the pooled kernels take <= 64 bins and pass
-    wider ones on (ST_DEFER_HIST64, ST_DEFER_HIST); all of them against the oracle."""
-    b = wide_histogram_batch(60, 5)
+    wider ones on (ST_DEFER_HIST64, ST_DEFER_HIST, ST_DEFER_WIDE); all of them against the
+    oracle, none left unscored."""
+    from oracle.bates import backward_diff, fd_bins
+
+    b = wide_histogram_batch(80, 5)
+    widest = max(max(fd_bins(p.astype(np.int64)), fd_bins(backward_diff(p.astype(np.int64))))
+                 for p in b["prof"])
+    assert widest > 1024, widest
     out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     assert not (st & 0xFFFF0000).any(), "internal deferral bits left in status"
-    ref, rst, own = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert not (st & 0x10).any(), "PFE_ST_UNSUPPORTED"
+    ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
-    check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor)
+    check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor, rmax=rmax,
+                  stable_slack=1)
 
 
 def test_pooled_tiny_and_empty_batches(engine):

@@ -31,7 +31,8 @@ def test_lyon8_oracle_bit_exact(name):
     assert np.array_equal(got[m], ref[m])
 
 
-@pytest.mark.parametrize("name,rows", [("bates22_phcx128", 90), ("bates22_superb64", 45)])
+@pytest.mark.parametrize("name,rows", [("bates22_phcx128", 90), ("bates22_superb64", 45),
+                                       ("bates22_phcx128_wide", 20)])
 def test_bates22_oracle_vs_reference(name, rows):
     d = load(name)
     prof, sub, curve, scal = bates_inputs(d)

@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle.bates as B  # noqa: E402
 from golden_util import bates_inputs, load  # noqa: E402
 
-SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128")
+SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide")
 
 
 def nudger(orig, steps):

@@ -241,7 +241,26 @@ SPECS = [
     ("bates22_phcx128_nsub32", "bates22", False, 60, 128, 128, 32, 128, 128, 7),
     # config 5's 30-column matrix: 8 Lyon features then the 22 scores of the same files
     ("all30_phcx128", "all30", False, 80, 128, 128, 16, 128, 128, 8),
+    # near-flat profiles quantised from sigma ~ 0.5 noise under a narrow pulse: tiny
+    # interquartile ranges, so Freedman-Diaconis histograms of 1000-1600 bins (rows 8..39)
+    ("bates22_phcx128_wide", "bates22", False, 48, 128, 128, 16, 128, 128, 9),
 ]
+
+
+def lownoise_wide_rows(rng, n, lp):
+    """Profiles whose profile or derivative histogram has more than 1024 FD bins."""
+    from oracle.bates import backward_diff, fd_bins
+
+    x = np.arange(lp)
+    rows = []
+    while len(rows) < n:
+        base = rng.normal(100, 0.5, lp)
+        mu, w = rng.uniform(10, lp - 10), rng.uniform(1.0, 3.0)
+        p = np.clip(np.rint(base + 150 * np.exp(-0.5 * ((x - mu) / w) ** 2)), 0, 255)
+        p = p.astype(np.int64)
+        if max(fd_bins(p), fd_bins(backward_diff(p))) > 1024:
+            rows.append(p.astype(np.uint8))
+    return np.stack(rows)
 
 
 def main(only=None):
@@ -278,6 +297,8 @@ def main(only=None):
             else:
                 prof, sub, curve, blocks, period, dmv, snr, width = bates_set(
                     rng, n, lp, nsub, lsb, ndm, superb)
+                if name.endswith("_wide"):
+                    prof[8:] = lownoise_wide_rows(rng, n - 8, lp)
                 b0 = blocks if superb else _rows_lyon(rng, n, 128)
                 arrays = dict(n=n, prof=prof, sub=sub, block0=b0, block1=blocks,
                               period=period, dm=dmv, snr=snr, width=width,
@@ -366,6 +387,57 @@ def make_pfd_golden(manifest):
                                       "patches": {k: [a for a, _ in v] for k, v in PFD_PATCHES.items()}}
 
 
+LABEL_RUNNER = r'''
+import sys, warnings
+warnings.simplefilter("ignore")
+import DataProcessor
+dp = DataProcessor.DataProcessor(False)
+# DataProcessor.label (:691-826) with the regexes labelPHCX / labelPFD pass (labelPFD itself
+# cannot be called with the two arguments ScoreGenerator.py:225 gives it)
+regex = [dp.phcxRegex] if sys.argv[2] == "phcx" else [dp.pfdRegex, dp.pfdScrunchedRegex]
+dp.label(sys.argv[1], False, regex)
+'''
+
+
+def make_label_golden(manifest):
+    """--label mode: the four files DataProcessor.label writes for a directory of PHCX files
+    and one of PFD files (text, with the directory prefix replaced by '<DIR>')."""
+    from pulsarfeatureextractor_amd import pfd
+
+    with tempfile.TemporaryDirectory(prefix="pfe_golden_label_") as tmp:
+        refdir = build_reference(tmp)
+        with open(os.path.join(refdir, "_label_runner.py"), "w") as f:
+            f.write(LABEL_RUNNER)
+        out = {}
+        # PHCX: 20 candidates of the 22-score recipe (rows 0, 3, 4 fail)
+        rng = np.random.default_rng(20261015 + 100 * 10)
+        prof, sub, curve, blocks, period, dmv, snr, width = bates_set(rng, 20, 128, 16, 128, 128, False)
+        arrays = dict(n=20, prof=prof, sub=sub, block0=_rows_lyon(rng, 20, 128), block1=blocks,
+                      period=period, dm=dmv, snr=snr, width=width, dm_start=0.0, dm_end=200.0,
+                      n_dm_index=101)
+        d = os.path.join(tmp, "label_phcx")
+        write_files(d, "label", arrays, False)
+        subprocess.run([sys.executable, "_label_runner.py", d, "phcx"], cwd=refdir, check=True,
+                       env=dict(os.environ, MPLBACKEND="Agg"), capture_output=True)
+        for k in ("Scores.csv", "Profile.csv", "DMCurve.csv", "Cands.meta"):
+            out["phcx_" + k] = open(os.path.join(d, k)).read().replace(d, "<DIR>")
+        for k, v in arrays.items():
+            out["phcx_in_" + k] = np.asarray(v)
+        # PFD: the first 12 folds of the pfd_64x16 recipe
+        d = os.path.join(tmp, "label_pfd")
+        os.makedirs(d)
+        for i, (c, kw) in enumerate(pfd_candidates(12, 8, 16, 64, 20261915)):
+            pfd.write(os.path.join(d, f"label_{i:04d}.pfd"), **c, **kw)
+        subprocess.run([sys.executable, "_label_runner.py", d, "pfd"], cwd=refdir, check=True,
+                       env=dict(os.environ, MPLBACKEND="Agg"), capture_output=True)
+        for k in ("Scores.csv", "Profile.csv", "DMCurve.csv", "Cands.meta"):
+            out["pfd_" + k] = open(os.path.join(d, k)).read().replace(d, "<DIR>")
+        np.savez_compressed(os.path.join(GOLDEN, "label.npz"), **out)
+        manifest["sets"]["label"] = {"mode": "DataProcessor.label", "phcx_seed": 20261015 + 1000,
+                                     "phcx_n": 20, "pfd_seed": 20261915, "pfd_n": 12,
+                                     "pfd_shape": [8, 16, 64]}
+
+
 def _rows_lyon(rng, n, L):
     from pulsarfeatureextractor_amd.synth import _rows_numpy
 
@@ -377,6 +449,12 @@ if __name__ == "__main__":
         mpath = os.path.join(GOLDEN, "manifest.json")
         man = json.load(open(mpath))
         make_pfd_golden(man)
+        with open(mpath, "w") as f:
+            json.dump(man, f, indent=1)
+    elif "--label" in sys.argv:  # the --label golden only
+        mpath = os.path.join(GOLDEN, "manifest.json")
+        man = json.load(open(mpath))
+        make_label_golden(man)
         with open(mpath, "w") as f:
             json.dump(man, f, indent=1)
     elif "--only" in sys.argv:  # regenerate the named PHCX sets only, keep the others
