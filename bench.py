@@ -508,8 +508,11 @@ def run_subband(ctx, args, n, lsb, steps, warmup):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "pfe::k_subband2<4, uint16_t, 4>",
+            "kernel": f"pfe::k_subband_fast<{lsb}, 4>",
             "algorithmic_bytes_per_candidate": per_cand,
+            "note": "bytes-based roofline for comparability; the kernel is VALU-issue bound "
+                    "(about 2.2k wave instructions per candidate, 3 waves/SIMD at 159 VGPRs), "
+                    "see DESIGN.md section 3.3",
             "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
         },
     }, out
