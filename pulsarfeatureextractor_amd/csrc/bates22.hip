@@ -54,15 +54,16 @@ static int persistent_waves(int64_t n) {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// hand-over regions (lm_group.h HandOver) of the three chains: waves x slots x K x 16 lanes;
-// the Gaussian chain runs a.pwaves waves, the DM and sine kernels pool_grid(a, 3)
+// hand-over regions (lm_group.h HandOver) of the three chains: waves x slots x K x group
+// lanes (16; 32 for the profile fits of > 128 bins); the Gaussian chain runs a.pwaves waves,
+// the DM and sine kernels pool_grid(a, 3)
 static int64_t hand_waves(int64_t n, int region) {
   const int64_t cap = (int64_t)device_cus() * (region == HAND_GAUSS ? 8 : 12);
   return n < 1 ? 1 : n < cap ? n : cap;
 }
-static size_t hand_bytes(int64_t n, int region) {
+static size_t hand_bytes(int64_t n, int region, int lp) {
   const int k = region == HAND_GAUSS ? HAND_K_GAUSS : region == HAND_DM ? HAND_K_DM : HAND_K_SINE;
-  return (size_t)hand_waves(n, region) * GLM_FPW * k * 16 * sizeof(double);
+  return (size_t)hand_waves(n, region) * GLM_FPW * k * glm_group_lanes(lp) * sizeof(double);
 }
 
 // waves of k_ghist_wide (each with a WIDE_SLAB_BYTES scratch slab)
@@ -72,7 +73,7 @@ static int wide_waves(int64_t n) { return (int)(n < 256 ? (n > 0 ? n : 1) : 256)
 // [per-wave scratch]
 size_t bates22_workspace_bytes(const pfe_bates_in* in) {
   size_t hb = 0;
-  for (int r = 0; r < 3; ++r) hb += align256(hand_bytes(in->n, r));
+  for (int r = 0; r < 3; ++r) hb += align256(hand_bytes(in->n, r, in->lp));
   return 256 + align256((size_t)in->n * sizeof(GaussWS)) +
          align256(BATES_NCOUNTERS * sizeof(unsigned)) + hb +
          align256((size_t)in->n * sizeof(int)) + (size_t)wide_waves(in->n) * WIDE_SLAB_BYTES +
@@ -100,7 +101,7 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work, const Options& o) 
   const bool ho = o.handover != 0;
   for (int r = 0; r < 3; ++r) {
     a.hand[r] = ho ? (double*)wb : nullptr;
-    wb += align256(hand_bytes(n, r));
+    wb += align256(hand_bytes(n, r, lp));
   }
   a.wide_list = (int*)wb;
   wb += align256((size_t)n * sizeof(int));

@@ -73,6 +73,10 @@ constexpr int BATES_NCOUNTERS = 16;
 // hand_waves() waves; a kernel whose functor needs more re-evaluates instead.
 enum : int { HAND_GAUSS = 0, HAND_DM = 1, HAND_SINE = 2 };
 constexpr int HAND_K_GAUSS = 24, HAND_K_DM = 24, HAND_K_SINE = 8;
+// lanes per group of the pooled profile fits (lm_group.h): 16 up to 128 bins, 32 (8 rows per
+// lane) up to 256 -- larger profiles use the batched solver
+__host__ __device__ constexpr int glm_group_lanes(int lp) { return lp > 128 ? 32 : 16; }
+constexpr int GLM_MAX_LP = 256;
 
 // Side streams of a handle: the score groups that do not depend on each other run on them
 // concurrently with the caller's stream (sine fits | Gaussian chain | DM fit + sub-bands), so

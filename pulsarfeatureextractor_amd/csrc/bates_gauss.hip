@@ -1991,9 +1991,9 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
 // fit per lane.  Data rows of the fits in group layout: row r -> group-lane r % 16, slot r / 16.
 // ---------------------------------------------------------------------------------------
 // ---- s8, s9 -----------------------------------------------------------------------------
-template <int P, int FPW>
+template <int P, int FPW, int G>
 struct Gt1Prob {
-  static constexpr int MG = 4 * P;
+  static constexpr int MG = 64 * P / G;
   BatesArgs a;
   SlotTab<FPW>& T;
   int nslots;
@@ -2032,10 +2032,10 @@ struct Gt1Prob {
     GaussBgFn<MG> fn;
     const int64_t c = T.cand[f];
     const double minbg = a.ws[c].minbg, pstd = a.ws[c].pstd;
-    const int lp = a.lp, cut = lp / 2, gl = glane();
+    const int lp = a.lp, cut = lp / 2, gl = glane<G>();
 #pragma unroll
     for (int k = 0; k < MG; ++k) {
-      const int i = gl + GLM_G * k;
+      const int i = gl + G * k;
       const bool ok = i < lp;
       fn.ok[k] = ok;
       fn.x[k] = (double)i;
@@ -2059,18 +2059,19 @@ struct Gt1Prob {
 template <int P>
 __global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
   constexpr int FPW = GLM_FPW;
+  constexpr int G = glm_group_lanes(64 * P);
   __shared__ BlmState<4, FPW> S;
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gt1Prob<P, FPW> prob{a, T, a.gslots};
-  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  Gt1Prob<P, FPW, G> prob{a, T, a.gslots};
+  glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the 8 peel passes ----------------------------------------------------------
-template <int P, int FPW>
+template <int P, int FPW, int G>
 struct PeelProb {
-  static constexpr int MG = 4 * P;
+  static constexpr int MG = 64 * P / G;
   BatesArgs a;
   SlotTab<FPW>& T;
   double* xs;  // wave scratch: x rows of the slots, [FPW][64P]
@@ -2159,13 +2160,13 @@ struct PeelProb {
   }
   __device__ __forceinline__ GaussAbsBgFn<MG> load(int f) const {
     GaussAbsBgFn<MG> fn;
-    const int gl = glane();
+    const int gl = glane<G>();
     const int mp = T.mpad[f];
     const double* X = xs + (size_t)f * 64 * P;
     const double* Y = yv + (size_t)f * 64 * P;
 #pragma unroll
     for (int k = 0; k < MG; ++k) {
-      const int r = gl + GLM_G * k;
+      const int r = gl + G * k;
       fn.x[k] = X[r];
       fn.y[k] = Y[r];
       fn.ok[k] = r < mp;
@@ -2186,14 +2187,17 @@ __global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
   blm_sync();
   double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   double* yv = xs + (size_t)FPW * 64 * P;
-  PeelProb<P, FPW> prob{a, T, xs, yv, ys, cx, a.gslots};
-  glm_engine<4, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  constexpr int G = glm_group_lanes(64 * P);
+  PeelProb<P, FPW, G> prob{a, T, xs, yv, ys, cx, a.gslots};
+  glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the final 8-parameter fit ----------------------------------------------
-template <int P, int FPW>
+// G lanes per group: 16 keeps 4P rows per lane (8 at 128 bins: the 8 x 8 Jacobian block,
+// residuals and both exp caches), 32 halves that.
+template <int P, int FPW, int G>
 struct Gdg8Prob {
-  static constexpr int MG = 4 * P;
+  static constexpr int MG = 64 * P / G;
   BatesArgs a;
   SlotTab<FPW>& T;
   int nslots;
@@ -2229,11 +2233,11 @@ struct Gdg8Prob {
   }
   __device__ __forceinline__ DoubleGaussFn<MG> load(int f) const {
     DoubleGaussFn<MG> dg;
-    const int L = a.lp, cut = L / 2, gl = glane();
+    const int L = a.lp, cut = L / 2, gl = glane<G>();
     const int64_t row = T.cand[f] * L;
 #pragma unroll
     for (int k = 0; k < MG; ++k) {
-      const int i = gl + GLM_G * k;
+      const int i = gl + G * k;
       const bool ok = i < L;
       dg.x[k] = (double)i;
       dg.y[k] = ok ? prof_at(a, row + (i + cut) % L) : 0.0;
@@ -2247,12 +2251,15 @@ struct Gdg8Prob {
 template <int P>
 __global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
   constexpr int FPW = GLM_FPW;
+  // 16 lanes (8 rows each) at 128 bins: 32 lanes measured 7 % slower there
+  // (profiles/r02_gdg8_g32_ab.txt); 32 lanes (8 rows each) at 256 bins
+  constexpr int G = glm_group_lanes(64 * P);
   __shared__ BlmState<8, FPW> S;
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gdg8Prob<P, FPW> prob{a, T, a.gslots};
-  glm_engine<8, 4 * P, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  Gdg8Prob<P, FPW, G> prob{a, T, a.gslots};
+  glm_engine<8, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- launchers -----------------------------------------------------------------------
@@ -2262,19 +2269,19 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
   const int L = a.lp;
   // batched lmdif (lm_batch.h) unless the handle selects the wave-per-fit kernels
   const bool use_blm = a.solver != PFE_SOLVER_WAVE;
-  // pooled group-LM kernels (lm_group.h) for <= 128 bins (the default solver)
-  const bool use_glm = a.solver == PFE_SOLVER_POOLED && L <= 128;
+  // pooled group-LM kernels (lm_group.h) for <= 256 bins (the default solver)
+  const bool use_glm = a.solver == PFE_SOLVER_POOLED && L <= GLM_MAX_LP;
   const dim3 pool((unsigned)a.pwaves);
 #define PFE_GAUSS_LAUNCH(P)                                                             \
   do {                                                                                  \
     if (use_glm && a.fprof) {                                                           \
-      hipLaunchKernelGGL((k_ghistg<(P <= 2 ? P : 2), true>), pool, dim3(64), 0, st, a); \
-      hipLaunchKernelGGL((k_gfixg<(P <= 2 ? P : 2), true>), pool, dim3(64), 0, st, a);  \
+      hipLaunchKernelGGL((k_ghistg<(P <= 4 ? P : 4), true>), pool, dim3(64), 0, st, a); \
+      hipLaunchKernelGGL((k_gfixg<(P <= 4 ? P : 4), true>), pool, dim3(64), 0, st, a);  \
       hipLaunchKernelGGL((k_ghist<P, 4, false, true, true>), gw(a.n), dim3(BLOCK), 0, st, a); \
       hipLaunchKernelGGL((k_ghist<P, 16, true, true>), gw(a.n), dim3(BLOCK), 0, st, a);  \
     } else if (use_glm) {                                                               \
-      hipLaunchKernelGGL((k_ghistg<(P <= 2 ? P : 2), false>), pool, dim3(64), 0, st, a); \
-      hipLaunchKernelGGL((k_gfixg<(P <= 2 ? P : 2), false>), pool, dim3(64), 0, st, a);  \
+      hipLaunchKernelGGL((k_ghistg<(P <= 4 ? P : 4), false>), pool, dim3(64), 0, st, a); \
+      hipLaunchKernelGGL((k_gfixg<(P <= 4 ? P : 4), false>), pool, dim3(64), 0, st, a);  \
       hipLaunchKernelGGL((k_ghist<P, 4, false, false, true>), gw(a.n), dim3(BLOCK), 0, st, a); \
       hipLaunchKernelGGL((k_ghist<P, 16, true, false>), gw(a.n), dim3(BLOCK), 0, st, a); \
     } else if (a.fprof) {                                                               \
@@ -2290,20 +2297,20 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
     else                                                                                \
       hipLaunchKernelGGL((k_ghist_wide<P, false>), dim3((unsigned)a.wide_waves), dim3(64), 0, st, a); \
     if (use_glm)                                                                        \
-      hipLaunchKernelGGL((k_gt1g<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                        \
+      hipLaunchKernelGGL((k_gt1g<(P <= 4 ? P : 4)>), pool, dim3(64), 0, st, a);                        \
     else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gt1b<P>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)),      \
                          dim3(64), 0, st, a);                                           \
     else                                                                                \
       hipLaunchKernelGGL((k_gt1<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
     if (use_glm)                                                                        \
-      hipLaunchKernelGGL((k_gdgg<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                        \
+      hipLaunchKernelGGL((k_gdgg<(P <= 4 ? P : 4)>), pool, dim3(64), 0, st, a);                        \
     else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gdgb<P>), dim3((unsigned)a.pwaves), dim3(64), 0, st, a);    \
     else                                                                                \
       hipLaunchKernelGGL((k_gdg<P>), gw(a.n), dim3(BLOCK), 0, st, a);                   \
     if (use_glm)                                                                        \
-      hipLaunchKernelGGL((k_gdg8g<(P <= 2 ? P : 2)>), pool, dim3(64), 0, st, a);                       \
+      hipLaunchKernelGGL((k_gdg8g<(P <= 4 ? P : 4)>), pool, dim3(64), 0, st, a);                       \
     else if (use_blm)                                                                   \
       hipLaunchKernelGGL((k_gdg8b<P, BLM_FPW>), dim3((unsigned)((a.n + a.fpw - 1) / a.fpw)), \
                          dim3(64), 0, st, a);                                           \

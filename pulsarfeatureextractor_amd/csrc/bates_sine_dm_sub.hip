@@ -276,9 +276,9 @@ struct SineAnyFn {  // SineFn<MPL, sqr> with the model chosen per slot
   }
 };
 
-template <int MPL, bool F, int FPW>
+template <int MPL, bool F, int FPW, int G>
 struct SineProb {
-  static constexpr int MG = 4 * MPL;
+  static constexpr int MG = 64 * MPL / G;
   BatesArgs a;
   SlotTab<FPW>& T;  // d0 = h, d1 = y0, mpad = maxima, pass = 0 (sine) / 1 (sine^2)
   double* sg;       // LDS stage (F)
@@ -353,10 +353,10 @@ struct SineProb {
   __device__ __forceinline__ SineAnyFn<MG> load(int f) const {
     SineAnyFn<MG> fn;
     const int64_t c = T.cand[f];
-    const int lp = a.lp, gl = glane();
+    const int lp = a.lp, gl = glane<G>();
 #pragma unroll
     for (int k = 0; k < MG; ++k) {
-      const int i = gl + GLM_G * k;
+      const int i = gl + G * k;
       fn.ok[k] = i < lp;
       fn.x[k] = (double)i;
       fn.y[k] = fn.ok[k] ? prof_at(a, c * lp + i) : 0.0;
@@ -377,8 +377,9 @@ __global__ __launch_bounds__(64, 3) void k_sineg(BatesArgs a) {
   __shared__ double stage[F ? 64 * MPL : 1];
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  SineProb<MPL, F, FPW> prob{a, T, stage, a.gslots};
-  glm_engine<2, 4 * MPL, FPW>(prob, S, T.ph, T.list, a.hand[HAND_SINE], HAND_K_SINE);
+  constexpr int G = glm_group_lanes(64 * MPL);
+  SineProb<MPL, F, FPW, G> prob{a, T, stage, a.gslots};
+  glm_engine<2, 64 * MPL / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_SINE], HAND_K_SINE);
 }
 
 // ======================================================================================
@@ -629,11 +630,13 @@ static bool glm_on(const BatesArgs& a) { return a.solver == PFE_SOLVER_POOLED; }
 
 template <bool F>
 static void launch_sine_t(const BatesArgs& a, hipStream_t st) {
-  if (glm_on(a) && a.lp <= 128) {
+  if (glm_on(a) && a.lp <= GLM_MAX_LP) {
     if (a.lp <= 64)
       hipLaunchKernelGGL((k_sineg<1, F>), pool_grid(a, 3), dim3(64), 0, st, a);
-    else
+    else if (a.lp <= 128)
       hipLaunchKernelGGL((k_sineg<2, F>), pool_grid(a, 3), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_sineg<4, F>), pool_grid(a, 3), dim3(64), 0, st, a);
     return;
   }
   if (a.lp <= 64)

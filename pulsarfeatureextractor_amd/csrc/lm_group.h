@@ -9,7 +9,9 @@
 //   * a wave owns FPW fit SLOTS; the state of each lives in LDS (BlmState, [element][slot]);
 //   * the m-parallel half runs in GROUPS of G = 16 lanes (one DPP row): NG = 4 fits are
 //     worked at once, row r of a fit in group-lane r % 16, register slot r / 16; reductions
-//     are 4 DPP steps inside the row and broadcasts are row_newbcast -- no cross-row traffic;
+//     are 4 DPP steps inside the row and broadcasts are row_newbcast -- no cross-row traffic.
+//     G = 32 (two DPP rows, NG = 2) halves the rows each lane holds (the 8-parameter fit's
+//     registers, 256-bin profiles): one v_permlane16_swap step joins the two rows;
 //   * the serial half (gtol test, lmpar, predicted reduction) runs one fit per lane (SIMT,
 //     blm_simt of lm_batch.h, unchanged);
 //   * slots are refilled as soon as their fit ends (Problem::refill, wave-cooperative), so
@@ -31,22 +33,46 @@
 
 namespace pfe {
 
-constexpr int GLM_G = 16;  // lanes per group: one DPP row
+constexpr int GLM_G = 16;  // lanes per group: one DPP row (default; 32 = two rows)
 
 enum : int { PH_EMPTY = 0, PH_INIT = 1, PH_OUTER = 2, PH_LMPAR = 3, PH_TRIAL = 4, PH_DONE = 5 };
 
-__device__ __forceinline__ int glane() { return lane_id() & (GLM_G - 1); }
+template <int G = GLM_G>
+__device__ __forceinline__ int glane() {
+  static_assert(G == 16 || G == 32, "groups of one or two DPP rows");
+  return lane_id() & (G - 1);
+}
 
-// sum over the 16 lanes of a DPP row; every lane of the row gets the same bits (IEEE
-// addition is commutative, so the mirrored butterflies agree)
+// v_permlane16_swap of v with itself: .even holds the even row's value of each row pair
+// (rows 0,1 -> row 0's), .odd the odd row's
+struct RowPair {
+  double even, odd;
+};
+__device__ __forceinline__ RowPair row_pair(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)b, hi = (unsigned)((unsigned long long)b >> 32);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return {__longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0])),
+          __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]))};
+}
+
+// sum over the G lanes of a group; every lane of the group gets the same bits (IEEE
+// addition is commutative, so the mirrored butterflies agree, and both rows of a pair add
+// the same two row sums)
+template <int G = GLM_G>
 __device__ __forceinline__ double gsum(double v) {
   v += dpp_f64<DPP_QUAD_XOR1>(v);
   v += dpp_f64<DPP_QUAD_XOR2>(v);
   v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
   v += dpp_f64<DPP_ROW_MIRROR>(v);
+  if constexpr (G == 32) {
+    const RowPair r = row_pair(v);
+    v = r.even + r.odd;
+  }
   return v;
 }
-template <int K>
+template <int K, int G = GLM_G>
 __device__ __forceinline__ void gsum_from(double (&v)[K], int lo) {
 #pragma unroll
   for (int k = 0; k < K; ++k)
@@ -60,6 +86,14 @@ __device__ __forceinline__ void gsum_from(double (&v)[K], int lo) {
 #pragma unroll
   for (int k = 0; k < K; ++k)
     if (k >= lo) v[k] += dpp_f64<DPP_ROW_MIRROR>(v[k]);
+  if constexpr (G == 32) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k >= lo) {
+        const RowPair r = row_pair(v[k]);
+        v[k] = r.even + r.odd;
+      }
+  }
 }
 
 // value of group-lane j (row_newbcast; j folds to a constant inside unrolled loops)
@@ -68,7 +102,7 @@ __device__ __forceinline__ double nbc(double v) {
   return __longlong_as_double(
       __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xF, 0xF, false));
 }
-__device__ __forceinline__ double gbcast(double v, int j) {
+__device__ __forceinline__ double gbcast16(double v, int j) {
   switch (j) {
     case 0: return nbc<0>(v);
     case 1: return nbc<1>(v);
@@ -88,22 +122,31 @@ __device__ __forceinline__ double gbcast(double v, int j) {
     default: return nbc<15>(v);
   }
 }
+// value of group-lane j < 16 (a row of the group's first DPP row) in every lane of the group
+template <int G = GLM_G>
+__device__ __forceinline__ double gbcast(double v, int j) {
+  const double w = gbcast16(v, j);
+  if constexpr (G == 32)
+    return row_pair(w).even;
+  else
+    return w;
+}
 
 // Euclidean norm of a group-distributed m-vector (rows outside [0,m) hold 0)
-template <int MPL>
+template <int MPL, int G = GLM_G>
 __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
   double p = 0.0;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) p += f[k] * f[k];
-  return sqrt(gsum(p));
+  return sqrt(gsum<G>(p));
 }
 
-// qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%16, slot r/16)
-template <int N, int MPL>
+// qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%G, slot r/G)
+template <int N, int MPL, int G = GLM_G>
 __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
                                         double (&acnorm)[N]) {
-  static_assert(N <= GLM_G, "diagonal rows must sit in slot 0");
-  const int gl = glane();
+  static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
+  const int gl = glane<G>();
   double wa[N];
   {
     double s[N];
@@ -114,7 +157,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       for (int k = 0; k < MPL; ++k) p += a[k][j] * a[k][j];
       s[j] = p;
     }
-    gsum_from(s, 0);
+    gsum_from<N, G>(s, 0);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       acnorm[j] = sqrt(s[j]);
@@ -155,9 +198,9 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 #pragma unroll
     for (int k = 0; k < MPL; ++k)
       if (row_ge(gl, k, j)) p += a[k][j] * a[k][j];
-    double ajnorm = sqrt(gsum(p));
+    double ajnorm = sqrt(gsum<G>(p));
     if (ajnorm != 0.0) {
-      if (gbcast(a[0][j], j) < 0.0) ajnorm = -ajnorm;
+      if (gbcast<G>(a[0][j], j) < 0.0) ajnorm = -ajnorm;
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) a[k][j] = a[k][j] / ajnorm;
@@ -173,8 +216,8 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         }
         d[c] = q;
       }
-      gsum_from(d, j + 1);
-      const double ajj = gbcast(a[0][j], j);
+      gsum_from<N, G>(d, j + 1);
+      const double ajj = gbcast<G>(a[0][j], j);
 #pragma unroll
       for (int c = j + 1; c < N; ++c) {
         const double temp = d[c] / ajj;
@@ -182,7 +225,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
         if (rdiag[c] != 0.0) {
-          const double t2 = gbcast(a[0][c], j) / rdiag[c];
+          const double t2 = gbcast<G>(a[0][c], j) / rdiag[c];
           rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
           const double q = rdiag[c] / wa[c];
           if (0.05 * (q * q) <= EPSMCH) {
@@ -190,7 +233,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 #pragma unroll
             for (int k = 0; k < MPL; ++k)
               if (row_ge(gl, k, j + 1)) r += a[k][c] * a[k][c];
-            rdiag[c] = sqrt(gsum(r));
+            rdiag[c] = sqrt(gsum<G>(r));
             wa[c] = rdiag[c];
           }
         }
@@ -204,32 +247,33 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 // factors) to the slot's next O-phase, through per-wave global scratch laid out
 // [slot][word][group lane]: MINPACK's fvec = wa4 after a successful step, instead of
 // evaluating the function at the new x once more.  nullptr: re-evaluate (same bits).
-template <int MPL, class Fn>
+template <int MPL, class Fn, int G = GLM_G>
 struct HandOver {
   using Cache = typename FnCache<Fn>::type;
   static constexpr int CW = HasCols<Fn>::value ? (int)(sizeof(Cache) / sizeof(double)) : 0;
   static constexpr int K = MPL + CW;  // doubles per group lane per slot
+  static constexpr int WORDS = K * G;  // doubles per slot
   __device__ static __forceinline__ void put(double* hand, int f, const double (&fv)[MPL],
                                              const Cache& c) {
-    double* h = hand + (size_t)f * K * GLM_G + glane();
+    double* h = hand + (size_t)f * WORDS + glane<G>();
 #pragma unroll
-    for (int k = 0; k < MPL; ++k) h[k * GLM_G] = fv[k];
+    for (int k = 0; k < MPL; ++k) h[k * G] = fv[k];
     if constexpr (CW > 0) {
       double w[CW > 0 ? CW : 1];
       __builtin_memcpy(w, &c, sizeof(Cache));
 #pragma unroll
-      for (int i = 0; i < CW; ++i) h[(MPL + i) * GLM_G] = w[i];
+      for (int i = 0; i < CW; ++i) h[(MPL + i) * G] = w[i];
     }
   }
   __device__ static __forceinline__ void get(const double* hand, int f, double (&fv)[MPL],
                                              Cache& c) {
-    const double* h = hand + (size_t)f * K * GLM_G + glane();
+    const double* h = hand + (size_t)f * WORDS + glane<G>();
 #pragma unroll
-    for (int k = 0; k < MPL; ++k) fv[k] = h[k * GLM_G];
+    for (int k = 0; k < MPL; ++k) fv[k] = h[k * G];
     if constexpr (CW > 0) {
       double w[CW > 0 ? CW : 1];
 #pragma unroll
-      for (int i = 0; i < CW; ++i) w[i] = h[(MPL + i) * GLM_G];
+      for (int i = 0; i < CW; ++i) w[i] = h[(MPL + i) * G];
       __builtin_memcpy(&c, w, sizeof(Cache));
     }
   }
@@ -238,11 +282,11 @@ struct HandOver {
 // O-phase for slot f (one group): residuals at S.x (a fresh fit also initialises par, delta,
 // xnorm, the counters and fnorm), the forward-difference Jacobian, QR, Q^T f, R -> LDS.
 // Leaves info = -1 (the gtol test runs in the next SIMT phase).
-template <int N, int MPL, int FPW, class Fn>
+template <int N, int MPL, int FPW, int G = GLM_G, class Fn>
 __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>& S, bool fresh,
                                           const double* hand) {
   const double eps = 1.4901161193847656e-08;  // sqrt(max(epsfcn, epsmch)) = 2^-26
-  const int gl = glane();
+  const int gl = glane<G>();
   double x[N], fvec[MPL];
   typename FnCache<Fn>::type cache;
 #pragma unroll
@@ -250,13 +294,13 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   // the residuals at x: for an accepted step the trial's residuals, handed over or
   // recomputed (same function, same operands: the same bits)
   if (!fresh && hand)
-    HandOver<MPL, Fn>::get(hand, f, fvec, cache);
+    HandOver<MPL, Fn, G>::get(hand, f, fvec, cache);
   else
     fn_eval<Fn, N, MPL>(fcn, x, fvec, cache);
   int iter, nfev;
   double fnorm;
   if (fresh) {
-    fnorm = enorm_g(fvec);
+    fnorm = enorm_g<MPL, G>(fvec);
     iter = 1;
     nfev = 1;
   } else {
@@ -279,7 +323,7 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   nfev += N;
   int ipvt[N];
   double rdiag[N], acn[N];
-  qrfac_g<N, MPL>(fjac, ipvt, rdiag, acn);
+  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn);
   double diag[N];
   double xnorm = 0.0, delta = 0.0;
   if (iter == 1) {
@@ -303,20 +347,20 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const double ajj = gbcast(fjac[0][j], j);
+    const double ajj = gbcast<G>(fjac[0][j], j);
     if (ajj != 0.0) {
       double p = 0.0;
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) p += fjac[k][j] * wa4[k];
-      const double sum = gsum(p);
+      const double sum = gsum<G>(p);
       const double temp = -sum / ajj;
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) wa4[k] = wa4[k] + fjac[k][j] * temp;
     }
     if (gl == j) fjac[0][j] = rdiag[j];
-    qtf[j] = gbcast(wa4[0], j);
+    qtf[j] = gbcast<G>(wa4[0], j);
   }
 #pragma unroll
   for (int j = 0; j < N; ++j)
@@ -343,17 +387,17 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
 
 // T-phase for slot f (one group): evaluate the trial point, update delta/par, accept or
 // reject, convergence tests.  Returns the slot's next phase.
-template <int N, int MPL, int FPW, class Fn>
+template <int N, int MPL, int FPW, int G = GLM_G, class Fn>
 __device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>& S, int maxfev,
                                          double* hand) {
-  const int gl = glane();
+  const int gl = glane<G>();
   double wa2[N], wa4[MPL];
   typename FnCache<Fn>::type cache;
 #pragma unroll
   for (int j = 0; j < N; ++j) wa2[j] = S.trial[j][f];
   fn_eval<Fn, N, MPL>(fcn, wa2, wa4, cache);
   const int nfev = S.nfev[f] + 1;
-  const double fnorm1 = enorm_g(wa4);
+  const double fnorm1 = enorm_g<MPL, G>(wa4);
   double fnorm = S.fnorm[f];
   double delta = S.delta[f], par = S.par[f], xnorm = S.xnorm[f];
   const double pnorm = S.pnorm[f], prered = S.prered[f], dirder = S.dirder[f];
@@ -396,7 +440,7 @@ __device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>&
     if (delta <= EPSMCH * xnorm) info = 7;
     if (gnorm <= EPSMCH) info = 8;
   }
-  if (hand && accepted && info == 0) HandOver<MPL, Fn>::put(hand, f, wa4, cache);
+  if (hand && accepted && info == 0) HandOver<MPL, Fn, G>::put(hand, f, wa4, cache);
   if (gl == 0) {
     S.delta[f] = delta;
     S.par[f] = par;
@@ -432,16 +476,16 @@ __device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
   return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
 }
 
-// Hand the slots of `mask` to the groups, NG = 64/16 per round; body(f) runs in the group
+// Hand the slots of `mask` to the groups, NG = 64/G per round; body(f) runs in the group
 // that owns slot f (lanes of other groups are masked off).
-template <class Body>
+template <int G, class Body>
 __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body& body) {
   const int lane = lane_id();
   const int cnt = __builtin_popcountll(mask);
   if ((mask >> lane) & 1ull) list[__builtin_popcountll(mask & ((1ull << lane) - 1ull))] = lane;
   blm_sync();
-  const int g = lane / GLM_G;
-  for (int base = 0; base < cnt; base += 64 / GLM_G) {
+  const int g = lane / G;
+  for (int base = 0; base < cnt; base += 64 / G) {
     const int idx = base + g;
     if (idx < cnt) body(list[idx]);
   }
@@ -452,19 +496,20 @@ __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body&
 //   bool refill(int f, S)   -- finish slot f's previous fit if it had one (prob keeps that
 //                              state), then set up its next fit: start point in S.x[.][f];
 //                              false when the slot stays empty (work exhausted)
-//   Fn   load(int f) const  -- (one group) the residual functor of slot f, rows r = gl + 16k
+//   Fn   load(int f) const  -- (one group) the residual functor of slot f, rows r = gl + G k
 //   int  maxfev(int f) const
-// ph / list: LDS int[FPW] each.  hand_region: hand-over scratch of FPW x hand_k x GLM_G
-// doubles per wave (block), or nullptr.
-template <int N, int MPL, int FPW, class Prob>
+// ph / list: LDS int[FPW] each.  hand_region: hand-over scratch of FPW x hand_k x G doubles
+// per wave (block), or nullptr.  G: lanes per group (16 or 32; Prob::load lays the rows out
+// for the same G).
+template <int N, int MPL, int FPW, int G = GLM_G, class Prob>
 __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list,
                                            double* hand_region = nullptr, int hand_k = 0) {
   static_assert(FPW <= 64, "one slot per lane in the SIMT phase");
   const int lane = lane_id();
   using Fn = std::decay_t<decltype(prob.load(0))>;
-  constexpr int HK = HandOver<MPL, Fn>::K;
-  double* const hand = (hand_region && HK <= hand_k)
-                           ? hand_region + (size_t)blockIdx.x * FPW * hand_k * GLM_G
+  using HO = HandOver<MPL, Fn, G>;
+  double* const hand = (hand_region && HO::K <= hand_k)
+                           ? hand_region + (size_t)blockIdx.x * FPW * hand_k * G
                            : nullptr;
   if (lane < FPW) ph[lane] = PH_DONE;  // every slot takes its first fit in the refill step
   blm_sync();
@@ -497,9 +542,9 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // O-phase: fresh fits and accepted steps
     const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
     if (mo) {
-      glm_rounds(mo, list, [&](int f) {
+      glm_rounds<G>(mo, list, [&](int f) {
         const auto fn = prob.load(f);
-        glm_outer<N, MPL, FPW>(fn, f, S, ph[f] == PH_INIT, hand);
+        glm_outer<N, MPL, FPW, G>(fn, f, S, ph[f] == PH_INIT, hand);
       });
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
       blm_sync();
@@ -525,10 +570,10 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // T-phase
     const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
     if (mt) {
-      glm_rounds(mt, list, [&](int f) {
+      glm_rounds<G>(mt, list, [&](int f) {
         const auto fn = prob.load(f);
-        const int nph = glm_trial<N, MPL, FPW>(fn, f, S, prob.maxfev(f), hand);
-        if (glane() == 0) ph[f] = nph;
+        const int nph = glm_trial<N, MPL, FPW, G>(fn, f, S, prob.maxfev(f), hand);
+        if (glane<G>() == 0) ph[f] = nph;
       });
       // slots change groups between phases: the hand-over stores precede the next loads
       if (hand) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
