@@ -61,8 +61,10 @@ extern "C" {
 #define PFE_ST_DMFIT_FAIL     0x004u /* scores 16-19 raised          (PHCXFile.py:626-629) */
 #define PFE_ST_SUBBAND_FAIL   0x008u /* scores 20-22 raised          (PHCXFile.py:665-668) */
 #define PFE_ST_UNSUPPORTED    0x010u /* outside the shapes this build scores (a histogram with
-                                        more than 1024 Freedman-Diaconis bins); the row is not
-                                        scored */
+                                        more than 16384 Freedman-Diaconis bins).  Unreachable
+                                        for byte (PHCX) profiles of up to 32768 bins: their
+                                        non-zero IQR is a multiple of 0.25, so the bin count
+                                        is at most 510 n^(1/3).  The row is not scored */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu
@@ -96,8 +98,9 @@ int pfe_synchronize(pfe_handle* h);
  * bits of the LM-fitted scores (the m-sums are ordered differently); all others give
  * identical results and only change the schedule.
  *   PFE_OPT_SOLVER       (bits) LM solver of the 22-score kernels: PFE_SOLVER_POOLED
- *                        (default; pooled 16-lane-group engine for <= 128 bins, batched
- *                        beyond), PFE_SOLVER_BATCHED (one wave owns 32 fits), or
+ *                        (default; pooled group engine for <= 256 bins -- 16-lane groups up
+ *                        to 128 bins, 32-lane groups above -- batched beyond),
+ *                        PFE_SOLVER_BATCHED (one wave owns 32 fits), or
  *                        PFE_SOLVER_WAVE (one wave per fit; bit-identical to BATCHED)
  *   PFE_OPT_SERIAL       1: the independent score groups run in order on the handle's
  *                        stream instead of on its two side streams (default 0)

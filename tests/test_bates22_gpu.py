@@ -172,13 +172,14 @@ def test_batch_independence(engine):
         assert np.array_equal(np.nan_to_num(cat, nan=7.0), np.nan_to_num(full, nan=7.0))
 
 
-@pytest.mark.parametrize("lp", [128, 64])
-def test_pooled_group_solver(engine, lp):
-    """The pooled group-LM kernels (lm_group.h, the default for <= 128 bins) against the
-    batched wave kernels: same failures, bit-exact columns identical, the LM outputs
-    different only in the last bits of their m-sums (so at most at the reference's own
-    1-ulp chaos rates), and every fit's result independent of the pool it ran in."""
-    b = bates_batch(600, lp=lp, lsb=lp, seed=33 + lp)
+@pytest.mark.parametrize("lp,n", [(128, 600), (64, 600), (256, 300), (200, 200)])
+def test_pooled_group_solver(engine, lp, n):
+    """The pooled group-LM kernels (lm_group.h, the default for <= 256 bins: 16-lane groups up
+    to 128 bins, 32-lane groups above) against the batched wave kernels: same failures,
+    bit-exact columns identical, the LM outputs different only in the last bits of their
+    m-sums (so at most at the reference's own 1-ulp chaos rates), and every fit's result
+    independent of the pool it ran in."""
+    b = bates_batch(n, lp=lp, lsb=lp, seed=33 + lp)
     with engine.options(solver="batched"):
         o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
@@ -192,7 +193,7 @@ def test_pooled_group_solver(engine, lp):
         if j not in BITEXACT:
             assert (r[:, j] > 1e-5).mean() <= 1.5 * floor["moved_1e-5"][j] + 0.03, f"s{j + 1}"
     # pool independence: the same candidates in another order and batch size
-    perm = np.random.default_rng(1).permutation(len(b["prof"]))[:250]
+    perm = np.random.default_rng(1).permutation(len(b["prof"]))[:n * 5 // 12]
     o2, s2 = engine.bates22(b["prof"][perm], b["sub"][perm], b["dmcurve"][perm], b["scal"][perm])
     assert np.array_equal(s2, s1[perm])
     assert np.array_equal(np.nan_to_num(o2, nan=7.0), np.nan_to_num(o1[perm], nan=7.0))
