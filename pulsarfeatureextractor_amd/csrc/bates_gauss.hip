@@ -1985,10 +1985,11 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Pooled group-LM forms (lm_group.h) of the three fit kernels, for profiles of <= 128 bins:
+// Pooled group-LM forms (lm_group.h) of the three fit kernels, for profiles of <= 256 bins:
 // persistent waves keep GLM_FPW fit slots busy from a work queue of candidates; the
-// m-parallel half of lmdif runs in 16-lane groups (4 fits at a time), the serial half one
-// fit per lane.  Data rows of the fits in group layout: row r -> group-lane r % 16, slot r / 16.
+// m-parallel half of lmdif runs in groups of G lanes (16 up to 128 bins: 4 fits at a time;
+// 32 above: 2 fits at a time, glm_group_lanes), the serial half one fit per lane.  Data rows
+// of the fits in group layout: row r -> group-lane r % G, slot r / G.
 // ---------------------------------------------------------------------------------------
 // ---- s8, s9 -----------------------------------------------------------------------------
 template <int P, int FPW, int G>
