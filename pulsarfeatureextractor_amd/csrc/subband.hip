@@ -381,11 +381,36 @@ __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
 //     v_dot4 sums per 16-byte piece, taken in the same pass that builds the prefix sums;
 //   * s20 / s21: boxcar sums and their S, sum b^2 in integers; per-band reductions are
 //     reduce-scatters (16 bands over the 16 lanes of a row: 15 exchanges instead of 16 x 6);
-//     the s21 identity of k_subband2 with W_j = sum_i r_i b_ij accumulated by fma.
+//     the s21 identity of k_subband2 with W_j = sum_i r_i b_ij accumulated by fma;
+//   * no masks in the window loop: the prefix rows are padded with zero rows to a multiple of
+//     16 bands, and a window past the last one reads the same prefix twice, so its boxcar sum
+//     is 0 by construction and its key (0 << 10 | 1023 - j) loses to every real window
+//     (those have smaller j).
+__host__ __device__ constexpr int sb_pad16(int nsub) { return (nsub + 15) & ~15; }
 template <int LSB>
 __host__ __device__ constexpr size_t fast_wave_lds(int nsub) {
-  return ((size_t)nsub * sb_stride<uint16_t>(LSB) * 2 + 15) / 16 * 16 +
+  return ((size_t)sb_pad16(nsub) * sb_stride<uint16_t>(LSB) * 2 + 15) / 16 * 16 +
          ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16;
+}
+
+// inclusive scan of x over the SEG-lane segments of a DPP row (SEG <= 16): row_shr reads
+// 0 from outside the row, the select keeps a segment's scan inside it
+template <int SEG>
+__device__ __forceinline__ uint32_t seg_scan_incl(uint32_t x, int pos) {
+  if constexpr (SEG >= 2) {
+    const uint32_t o = (uint32_t)dpp_i32<0x111>((int)x);  // row_shr:1
+    x += (SEG == 16 || pos >= 1) ? o : 0u;
+  }
+  if constexpr (SEG >= 4) {
+    const uint32_t o = (uint32_t)dpp_i32<0x112>((int)x);  // row_shr:2
+    x += (SEG == 16 || pos >= 2) ? o : 0u;
+  }
+  if constexpr (SEG >= 8) {
+    const uint32_t o = (uint32_t)dpp_i32<0x114>((int)x);  // row_shr:4
+    x += (SEG == 16 || pos >= 4) ? o : 0u;
+  }
+  if constexpr (SEG >= 16) x += (uint32_t)dpp_i32<0x118>((int)x);  // row_shr:8
+  return x;
 }
 
 template <int M>
@@ -433,8 +458,12 @@ __device__ __forceinline__ int bitrev4(int l) {
   return ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
 }
 
+#ifndef PFE_SUBBAND_WPE
+#define PFE_SUBBAND_WPE 3  // 3 waves per SIMD at 256 bins (168 VGPRs)
+#endif
 template <int LSB, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PFE_SUBBAND_WPE)))
+void k_subband_fast(SubArgs a) {
   constexpr int SL = LSB >= 64 ? LSB / 64 : 1;  // window slots per lane
   constexpr int SEG = LSB / 16;                 // lanes per band in the 16-byte piece layout
   constexpr int STRIDE = sb_stride<uint16_t>(LSB);
@@ -445,9 +474,10 @@ __global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
   const int64_t c = (int64_t)blockIdx.x * WPB + w;
   if (c >= a.n) return;
   const int nsub = a.nsub;
+  const int npad = sb_pad16(nsub);
   unsigned char* wbase = sb_lds + w * fast_wave_lds<LSB>(nsub);
   uint16_t* E = reinterpret_cast<uint16_t*>(wbase);
-  int* bstat = reinterpret_cast<int*>(wbase + ((size_t)nsub * STRIDE * 2 + 15) / 16 * 16);
+  int* bstat = reinterpret_cast<int*>(wbase + ((size_t)npad * STRIDE * 2 + 15) / 16 * 16);
   int* maxbin = bstat + 3 * nsub;
 
   const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
@@ -460,6 +490,10 @@ __global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
   const int nw = LSB - wb + 1;
   const uint8_t* sb = a.sub + c * (int64_t)nsub * LSB;
   const int pos = lane & (SEG - 1);
+  // zero rows after the last band (read by the window loop's partial last block)
+  for (int t = nsub * STRIDE / 8 + lane; t < npad * STRIDE / 8; t += 64)
+    reinterpret_cast<uint32_t __attribute__((ext_vector_type(4)))*>(E)[t] =
+        (uint32_t __attribute__((ext_vector_type(4)))){0, 0, 0, 0};
   // this lane's 16 profile bytes (a piece sits at the same offset of its band every pass)
   uint32_t pw[4];
   {
@@ -495,13 +529,7 @@ __global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
       const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
       uint32_t e[16];
       const uint32_t tot = piece_prefix(wv, e);
-      uint32_t x = tot;
-#pragma unroll
-      for (int sft = 1; sft < SEG; sft <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)x, sft);
-        if (pos >= sft) x += o;
-      }
-      const uint32_t excl = x - tot;
+      const uint32_t excl = seg_scan_incl<SEG>(tot, pos) - tot;
       int X2 = 0, XP = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -554,25 +582,31 @@ __global__ __launch_bounds__(64 * WPB) void k_subband_fast(SubArgs a) {
   for (int k = 0; k < SL; ++k) W[k] = 0.0;
   double C = 0.0;
   int valid = 0;
+  // per window slot, band-independent: the prefix indices (a window past the last one reads
+  // E[lo] twice: b = 0) and the low half of the maximum key
+  int lo_k[SL], hi_k[SL], jk[SL];
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    const int j = lane + 64 * k;
+    lo_k[k] = j < LSB ? j : LSB;
+    hi_k[k] = j < nw ? j + wb : lo_k[k];
+    jk[k] = 1023 - j;
+  }
   for (int blk = 0; blk < nsub; blk += SB_NB) {
     const int nb = nsub - blk < SB_NB ? nsub - blk : SB_NB;
     int bv[SB_NB][SL];
     int sA[SB_NB], kA[SB_NB];
     unsigned long long qA[SB_NB];
+    const uint16_t* rows = E + blk * STRIDE;  // bands past nsub are the zero rows
 #pragma unroll
     for (int ii = 0; ii < SB_NB; ++ii) {
       int sv = 0, kmax = 0;
       unsigned long long qv = 0;
-      // branch-free: reads clamped into this wave's rows, out-of-range windows masked to 0
-      const uint16_t* row = E + (blk + ii < nsub ? blk + ii : nsub - 1) * STRIDE;
+      const uint16_t* row = rows + ii * STRIDE;
 #pragma unroll
       for (int k = 0; k < SL; ++k) {
-        const int j = lane + 64 * k;
-        const bool in = ii < nb && j < nw;
-        const int hi = j + wb < LSB ? j + wb : LSB;
-        int b = (int)row[hi] - (int)row[j < LSB ? j : LSB];
-        b = in ? b : 0;
-        const int kk = in ? ((b << 10) | (1023 - j)) : 0;
+        const int b = (int)row[hi_k[k]] - (int)row[lo_k[k]];
+        const int kk = (b << 10) | jk[k];
         kmax = kk > kmax ? kk : kmax;
         bv[ii][k] = b;
         sv += b;

@@ -32,6 +32,13 @@ def dump(path):
         for lp, n, seed in ((128, 20000, 77), (64, 20000, 78)):
             b = bates_batch(n, lp=lp, lsb=lp, seed=seed)
             sets[f"synth{lp}"] = (b["prof"], b["sub"], b["dmcurve"], b["scal"])
+        # pfe_subband3 (fast kernel: power-of-two nBins <= 256; nsub 20 = a partial block)
+        for nsub, lsb, n, seed in ((16, 256, 20000, 80), (20, 128, 8000, 81), (16, 64, 8000, 82),
+                                   (3, 32, 4000, 83), (40, 16, 4000, 84)):
+            b = bates_batch(n, lp=lsb, nsub=nsub, lsb=lsb, seed=seed)
+            out, st = e.subband3(b["prof"], b["sub"], b["scal"])
+            res[f"sub{nsub}x{lsb}_out"] = np.asarray(out)
+            res[f"sub{nsub}x{lsb}_st"] = np.asarray(st)
         for solver in ("pooled", "batched"):
             e.set_option("solver", solver)
             for name, args in sets.items():
