@@ -2,10 +2,16 @@
 """End-to-end throughput of the batched ScoreGenerator path: directory of PHCX files ->
 native parse -> pfe_bates22 / pfe_lyon8 on the GPU -> score text, phase by phase.
 
-  python tools/e2e_bench.py --n 4000 [--dir /tmp/pfe_e2e] [--workers 16]
+  python tools/e2e_bench.py --n 4000 [--dir /tmp/pfe_e2e] [--workers 16] [--mode phases|stream]
 
 The synthetic files follow SURVEY.md §8(d) (128-bin profile, 16x128 sub-bands, a
 128 x 128 DataBlock per section).  Writing them is not timed.
+
+--mode phases (default): parse everything, then score everything, phase by phase.
+--mode stream: the product path, DataProcessor.processPHCXCollectively -- batches of --batch
+files parsed on a helper thread one batch ahead of the GPU scoring, each batch's lines
+appended to the output in discovery order; reports the wall time and the process's peak RSS
+(run it in its own process so the peak is the streamed path's).
 """
 import argparse
 import json
@@ -42,6 +48,8 @@ def main():
     ap.add_argument("--n", type=int, default=4000)
     ap.add_argument("--dir", default="/tmp/pfe_e2e")
     ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--mode", choices=["phases", "stream"], default="phases")
+    ap.add_argument("--batch", type=int, default=8192)
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     have = sorted(f for f in os.listdir(args.dir) if f.endswith(".phcx.gz"))
@@ -52,6 +60,24 @@ def main():
     from pulsarfeatureextractor_amd.candidate import get_engine
 
     eng = get_engine(0)
+    if args.mode == "stream":
+        import resource
+        import tempfile
+
+        out = os.path.join(tempfile.mkdtemp(), "scores.csv")
+        dp = processor.DataProcessor(engine=eng, workers=args.workers, log=lambda *a: None,
+                                     batch=args.batch)
+        t0 = time.perf_counter()
+        dp.processPHCXCollectively(args.dir, False, out, False, False, False)
+        wall = time.perf_counter() - t0
+        with open(out) as f:
+            nlines = sum(1 for _ in f)
+        nfiles = len(processor.discover(args.dir, [processor.PHCX_RE]))
+        print(json.dumps({"mode": "stream", "files": nfiles, "batch": args.batch,
+                          "wall_s": wall, "files_per_s": nfiles / wall, "lines": nlines,
+                          "peak_rss_MB": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024,
+                          "workers": args.workers}))
+        return
     paths = processor.discover(args.dir, [processor.PHCX_RE])[: args.n]
     res = {"files": len(paths)}
     t0 = time.perf_counter()
