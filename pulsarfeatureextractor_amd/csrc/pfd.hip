@@ -505,6 +505,83 @@ __device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, con
   }
 }
 
+// The 100-DM chi^2 sweep of k_pfd_dmprof4 for L = 64 / 128 and nsub a multiple of 8 (the
+// PRESTO fold shapes): the same additions in the same order as the general loop below, with
+// less issue per LDS read.  A trial DM's rotation of sub-band j is wave-uniform, so lanes
+// 0-15 read the rotations of two DMs for 8 sub-bands at once and readlane makes them scalar;
+// the wrap (b + r) mod L is a mask; and each wave sweeps two DMs at a time (k, k + 4), four
+// independent ordered chains per lane.  numpy's pairwise leaf of the two chi^2 rows runs in
+// lanes 0-7 (DM k) and 8-15 (DM k + 4) together.
+template <int L>
+__device__ __forceinline__ void sweep_pow2(const double* T, const int* rot, int NS, int wv,
+                                           int lane, double avgprof, double varprof,
+                                           double* xb, float* chs, float* chis) {
+  constexpr int B = L / 64;  // bins per lane
+  static_assert(B == 1 || B == 2, "L = 64 or 128");
+  for (int k0 = wv; k0 < PFE_PFD_NDM; k0 += 8) {
+    const bool two = k0 + 4 < PFE_PFD_NDM;  // wave-uniform
+    const int k1 = two ? k0 + 4 : k0;
+    const int* ra = rot + k0 * NS;
+    const int* rb = rot + k1 * NS;
+    double s[2][B];
+    for (int j0 = 0; j0 < NS; j0 += 8) {
+      const int rv = lane < 8 ? ra[j0 + lane] : lane < 16 ? rb[j0 + lane - 8] : 0;
+      double v[2][8][B];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r0 = __builtin_amdgcn_readlane(rv, u);
+        const int r1 = __builtin_amdgcn_readlane(rv, 8 + u);
+        const double* row = T + (size_t)(j0 + u) * L;
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int b = lane + 64 * q;
+          v[0][u][q] = row[(b + r0) & (L - 1)];
+          v[1][u][q] = row[(b + r1) & (L - 1)];
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          double t = j0 == 0 ? v[d][0][q] : s[d][q] + v[d][0][q];
+#pragma unroll
+          for (int u = 1; u < 8; ++u) t = t + v[d][u][q];
+          s[d][q] = t;
+        }
+    }
+    // chi^2 terms of both DMs, then numpy's leaf: r_i = x[i] + x[i+8] + ... (L multiple of 8)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const double e = s[d][q] - avgprof;
+        xb[d * 128 + lane + 64 * q] = (e * e) / varprof;
+      }
+    lds_sync();
+    const double* xr = xb + ((lane >> 3) & 1) * 128;
+    double w[L / 8];
+#pragma unroll
+    for (int m = 0; m < L / 8; ++m) w[m] = xr[(lane & 7) + 8 * m];
+    double r = w[0];
+#pragma unroll
+    for (int m = 1; m < L / 8; ++m) r += w[m];
+    const double den = (double)L - 1.0;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int o = 8 * d;
+      const double r0 = bcast(r, o), r1 = bcast(r, o + 1), r2 = bcast(r, o + 2), r3 = bcast(r, o + 3);
+      const double r4 = bcast(r, o + 4), r5 = bcast(r, o + 5), r6 = bcast(r, o + 6), r7 = bcast(r, o + 7);
+      const double chi = (((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))) / den;
+      const int k = d ? k1 : k0;
+      if (lane == 0 && (d == 0 || two)) {
+        chs[k] = (float)chi;
+        if (chis) chis[k] = (float)chi;
+      }
+    }
+    lds_sync();
+  }
+}
+
 // Four-wave form of k_pfd_dmprof for profiles of <= 128 bins (the same arithmetic, bit for
 // bit).  The single-wave kernel streamed the fold with one dependent load per lane at a time
 // and swept the 100 trial DMs one after another; here
@@ -533,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   double* bv = sdb + NS;             // NS
   int* cum = (int*)(bv + NS);        // NS
   int* rot = cum + NS;               // PFE_PFD_NDM x NS accumulated rotations of the sweep
-  double* xbuf = bv + NS + ((PFE_PFD_NDM + 1) * NS + 1) / 2;  // 4 x 128, after cum and rot
+  double* xbuf = bv + NS + ((PFE_PFD_NDM + 1) * NS + 1) / 2;  // 4 x 256, after cum and rot
   __shared__ float chs[PFE_PFD_NDM], ftmp[PFE_PFD_NDM];
   const double* sc = a.scal + c * PFE_PFD_NSCAL;
   const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
@@ -598,8 +675,15 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   // takes every 4th trial DM; its lanes sum the rotated sub-band rows over the bins (a wave
   // reads 64 consecutive doubles of a row at a time), the chi^2 terms go to the wave's LDS
   // row and numpy's pairwise leaf sums them (np_leaf, lanes 0-7)
-  if (sweep) {
-    double* xb = xbuf + wv * 128;
+  if (sweep && (L == 128 || L == 64) && NS % 8 == 0) {
+    double* xb = xbuf + wv * 256;
+    float* chis = a.chis ? a.chis + c * PFE_PFD_NDM : nullptr;
+    if (L == 128)
+      sweep_pow2<128>(T, rot, NS, wv, lane, avgprof, varprof, xb, chs, chis);
+    else
+      sweep_pow2<64>(T, rot, NS, wv, lane, avgprof, varprof, xb, chs, chis);
+  } else if (sweep) {
+    double* xb = xbuf + wv * 256;
     const int b0 = lane, b1 = lane + 64;
     for (int k = wv; k < PFE_PFD_NDM; k += 4) {
       const int* rk = rot + k * NS;
@@ -686,7 +770,7 @@ size_t pfd_lds_bytes(int nsub, int L) {
 
 static size_t pfd4_lds_bytes(int nsub, int L) {
   return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int) + 8 +
-         4 * 128 * sizeof(double);
+         4 * 256 * sizeof(double);
 }
 
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {

@@ -65,7 +65,9 @@ def test_fresh_shapes_vs_oracle(engine, tmp_path):
     """Other fold shapes (long profiles: pairwise sums over several 128-blocks)."""
     from pulsarfeatureextractor_amd.synth import pfd_candidate
 
-    for npart, nsub, L in ((4, 8, 256), (6, 64, 96), (2, 3, 300)):
+    # (8, 16, 128), (4, 24, 64): the sweep's power-of-two fast path (sweep_pow2), its DM
+    # curve checked bit for bit
+    for npart, nsub, L in ((4, 8, 256), (6, 64, 96), (2, 3, 300), (8, 16, 128), (4, 24, 64)):
         files = []
         for i in range(4):
             c = pfd_candidate(np.random.default_rng(500 + i + L), npart, nsub, L)
@@ -78,6 +80,8 @@ def test_fresh_shapes_vs_oracle(engine, tmp_path):
             for i, d in enumerate(datas):
                 st = opfd.PFDState(d)
                 assert eq_nan(r["profile"][i], st.profile()).all(), (L, i)
+                chis = opfd.dm_curve(d)
+                assert np.array_equal(r["chis"][i], chis) or eq_nan(r["chis"][i], chis).all(), (L, i)
                 ref = np.array(opfd.lyon8_one(d))
                 got = r["lyon8"][i]
                 for j in (0, 1, 3, 4, 5, 7):

@@ -39,6 +39,22 @@ def dump(path):
             out, st = e.subband3(b["prof"], b["sub"], b["scal"])
             res[f"sub{nsub}x{lsb}_out"] = np.asarray(out)
             res[f"sub{nsub}x{lsb}_st"] = np.asarray(st)
+        # pfe_pfd_dmprof (fast sweep: L = 64/128 with nsub % 8 == 0; the others general) and
+        # pfe_pfd_bates22
+        from bench import pfd_block
+        from pulsarfeatureextractor_amd import pfd as _pfd
+
+        for shape in ((16, 32, 128), (8, 16, 64), (4, 8, 96), (4, 12, 128), (2, 40, 64)):
+            profs, subfreqs, pscal = _pfd.batch_inputs(pfd_block(64, shape, 9100 + shape[1]))
+            r = e.pfd_dmprof(profs, subfreqs, pscal)
+            tag = "pfd%dx%dx%d" % shape
+            res[f"{tag}_chis_out"] = np.asarray(r["chis"]).astype(np.float64)
+            res[f"{tag}_profile_out"] = np.asarray(r["profile"])
+            res[f"{tag}_lyon8_out"] = np.asarray(r["lyon8"])
+            res[f"{tag}_st"] = np.asarray(r["status"])
+            out, st = e.pfd_bates22(profs, subfreqs, pscal)
+            res[f"{tag}_b22_out"] = np.asarray(out)
+            res[f"{tag}_b22_st"] = np.asarray(st)
         for solver in ("pooled", "batched"):
             e.set_option("solver", solver)
             for name, args in sets.items():
