@@ -32,23 +32,76 @@ __device__ __forceinline__ double delay_from_dm(double dm, double f) {  // PFDOp
   return f > 0.0 ? dm / (0.000241 * f * f) : 0.0;
 }
 
+// numpy's pairwise sum of an LDS row with the leaf's loads issued before its adds when the
+// row is a single leaf (np_leaf128: the same order of additions, so the same bits)
+__device__ __forceinline__ double np_sum_row(const double* a, int n, int lane) {
+  return (n >= 8 && n <= 128) ? np_leaf128(a, n, lane) : np_pairwise<12>(a, n, lane);
+}
+
+// Python's builtin min (MAX = false) / max over an LDS row as a wave reduction: a[0] when
+// a[0] is NaN, else the first element equal (==) to the extreme of the rest -- what the
+// sequential scan with strict comparisons returns (py_min_seq / py_max_seq), ties and the
+// sign of zero included, since the pair (value, first index) is carried
+template <bool MAX>
+__device__ double py_ext_wave(const double* a, int n, int lane) {
+  const double a0 = a[0];
+  if (!(a0 == a0)) return a0;
+  double bv = a0;
+  int bi = 0;
+  for (int i = lane; i < n; i += 64) {
+    const double v = a[i];
+    if (MAX ? v > bv : v < bv) {
+      bv = v;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const double ov = __shfl_xor(bv, m);
+    const int oi = __shfl_xor(bi, m);
+    if ((MAX ? ov > bv : ov < bv) || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  return bv;
+}
+
+// numpy's float32 leaf sum of a short LDS row (np_leaf_f32) with the 8 accumulators in lanes
+// 0-7: the same additions in the same order, the result in every lane
+__device__ float np_leaf_f32_wave(const float* a, int n, int lane) {
+  if (n < 8) return np_leaf_f32(a, n);
+  const int nb = n - (n % 8);
+  float r = 0.0f;
+  if (lane < 8) {
+    r = a[lane];
+    for (int i = 8 + lane; i < nb; i += 8) r += a[i];
+  }
+  float q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), j));
+  float res = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  for (int i = nb; i < n; ++i) res += a[i];
+  return res;
+}
+
 // mean, std, skew, kurtosis of x[0..n) (LDS) as numpy.mean / numpy.std / scipy.stats.skew /
 // scipy.stats.kurtosis compute them in float64; tmp: n doubles of LDS scratch
 __device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double (&o)[4]) {
-  const double mean = np_pairwise<12>(x, n, lane) / (double)n;
+  const double mean = np_sum_row(x, n, lane) / (double)n;
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
     tmp[i] = d * d;
   }
   lds_sync();
-  const double m2 = np_pairwise<12>(tmp, n, lane) / (double)n;
+  const double m2 = np_sum_row(tmp, n, lane) / (double)n;
   lds_sync();
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
     tmp[i] = (d * d) * d;
   }
   lds_sync();
-  const double m3 = np_pairwise<12>(tmp, n, lane) / (double)n;
+  const double m3 = np_sum_row(tmp, n, lane) / (double)n;
   lds_sync();
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
@@ -56,7 +109,7 @@ __device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double
     tmp[i] = d2 * d2;
   }
   lds_sync();
-  const double m4 = np_pairwise<12>(tmp, n, lane) / (double)n;
+  const double m4 = np_sum_row(tmp, n, lane) / (double)n;
   lds_sync();
   const double eps = 2.220446049250313e-16;
   const double zl = eps * mean;
@@ -67,25 +120,32 @@ __device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double
   o[3] = zero ? NAN : m4 / (m2 * m2) - 3.0;
 }
 
-// the same in float32 (numpy on a float32 array), evaluated identically in every lane
-__device__ void stats4_f32(const float* a, float* tmp, int n, double (&o)[4]) {
-  const float mean = np_leaf_f32(a, n) / (float)n;
-  for (int i = 0; i < n; ++i) {
+// the same in float32 (numpy on a float32 array): the element passes spread over the lanes,
+// the leaf sums in lanes 0-7, the result in every lane
+__device__ void stats4_f32_wave(const float* a, float* tmp, int n, int lane, double (&o)[4]) {
+  const float mean = np_leaf_f32_wave(a, n, lane) / (float)n;
+  for (int i = lane; i < n; i += 64) {
     const float d = a[i] - mean;
     tmp[i] = d * d;
   }
-  const float m2 = np_leaf_f32(tmp, n) / (float)n;
-  for (int i = 0; i < n; ++i) {
+  lds_sync();
+  const float m2 = np_leaf_f32_wave(tmp, n, lane) / (float)n;
+  lds_sync();
+  for (int i = lane; i < n; i += 64) {
     const float d = a[i] - mean;
     tmp[i] = (d * d) * d;
   }
-  const float m3 = np_leaf_f32(tmp, n) / (float)n;
-  for (int i = 0; i < n; ++i) {
+  lds_sync();
+  const float m3 = np_leaf_f32_wave(tmp, n, lane) / (float)n;
+  lds_sync();
+  for (int i = lane; i < n; i += 64) {
     const float d = a[i] - mean;
     const float d2 = d * d;
     tmp[i] = d2 * d2;
   }
-  const float m4 = np_leaf_f32(tmp, n) / (float)n;
+  lds_sync();
+  const float m4 = np_leaf_f32_wave(tmp, n, lane) / (float)n;
+  lds_sync();
   const float zl = 1.1920929e-07f * mean;
   const bool zero = m2 <= zl * zl;
   o[0] = (double)mean;
@@ -93,7 +153,6 @@ __device__ void stats4_f32(const float* a, float* tmp, int n, double (&o)[4]) {
   o[2] = zero ? NAN : (double)(m3 / powf(m2, 1.5f));
   o[3] = zero ? NAN : (double)(m4 / (m2 * m2) - 3.0f);
 }
-
 
 // ---- the 22-score path: candidate parameters and sub-band scores ---------------------
 // CandidateFileInterface.filterScore(13|14) (CandidateFileInterface.py:97-107)
@@ -330,7 +389,7 @@ __device__ __forceinline__ void pfd_finish(const PfdArgs& a, int64_t c, double* 
   const int NS = a.nsub, L = a.L;
   if (a.lyon8) {
     double dmo[4] = {0.0, 0.0, 0.0, 0.0};
-    if (dm_ok) stats4_f32(chs, ftmp, PFE_PFD_NDM, dmo);
+    if (dm_ok) stats4_f32_wave(chs, ftmp, PFE_PFD_NDM, lane, dmo);
     if (lane == 0) {
       double* o = a.lyon8 + c * 8;
       for (int i = 0; i < 4; ++i) {
@@ -426,14 +485,14 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   }
   lds_sync();
   {
-    const double mn = py_min_seq(buf, L);
+    const double mn = py_ext_wave<false>(buf, L, lane);
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] - mn;  // normprof
     lds_sync();
-    const double mean = np_pairwise<12>(buf, L, lane) / (double)L;
+    const double mean = np_sum_row(buf, L, lane) / (double)L;
     lds_sync();
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] / mean;  // s
     lds_sync();
-    const double smin = py_min_seq(buf, L), smax = py_max_seq(buf, L);
+    const double smin = py_ext_wave<false>(buf, L, lane), smax = py_ext_wave<true>(buf, L, lane);
     lds_sync();
     for (int b = lane; b < L; b += 64) {
       const double t = (buf[b] - smin) / (smax - smin);
@@ -675,7 +734,12 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   // takes every 4th trial DM; its lanes sum the rotated sub-band rows over the bins (a wave
   // reads 64 consecutive doubles of a row at a time), the chi^2 terms go to the wave's LDS
   // row and numpy's pairwise leaf sums them (np_leaf, lanes 0-7)
+#if defined(PFE_PFD_PROBE) && PFE_PFD_PROBE == 1  // instrumented build: no sweep
+  if (sweep) {
+  } else if (false) {
+#else
   if (sweep && (L == 128 || L == 64) && NS % 8 == 0) {
+#endif
     double* xb = xbuf + wv * 256;
     float* chis = a.chis ? a.chis + c * PFE_PFD_NDM : nullptr;
     if (L == 128)
@@ -731,6 +795,9 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
     }
   }
   __syncthreads();
+#if defined(PFE_PFD_PROBE) && PFE_PFD_PROBE == 2  // instrumented build: no wave-0 tail
+  return;
+#endif
   if (wv != 0) return;
   // (the profile is built after the sweep: it does not feed it, and the wave-0-only calls it
   // makes kept out of the divergent part before the sweep)
@@ -743,14 +810,14 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
       buf[b] = s;
     }
     lds_sync();
-    const double mn = py_min_seq(buf, L);
+    const double mn = py_ext_wave<false>(buf, L, lane);
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] - mn;  // normprof
     lds_sync();
-    const double mean = np_pairwise<12>(buf, L, lane) / (double)L;
+    const double mean = np_sum_row(buf, L, lane) / (double)L;
     lds_sync();
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] / mean;  // s
     lds_sync();
-    const double smin = py_min_seq(buf, L), smax = py_max_seq(buf, L);
+    const double smin = py_ext_wave<false>(buf, L, lane), smax = py_ext_wave<true>(buf, L, lane);
     lds_sync();
     for (int b = lane; b < L; b += 64) {
       const double t = (buf[b] - smin) / (smax - smin);
