@@ -63,7 +63,8 @@ static int64_t hand_waves(int64_t n, int region) {
 }
 static size_t hand_bytes(int64_t n, int region, int lp) {
   const int k = region == HAND_GAUSS ? HAND_K_GAUSS : region == HAND_DM ? HAND_K_DM : HAND_K_SINE;
-  return (size_t)hand_waves(n, region) * GLM_FPW * k * glm_group_lanes(lp) * sizeof(double);
+  const int slots = region == HAND_GAUSS ? GDG8_FPW : GLM_FPW;  // the Gaussian chain's widest pool
+  return (size_t)hand_waves(n, region) * slots * k * glm_group_lanes(lp) * sizeof(double);
 }
 
 // waves of k_ghist_wide (each with a WIDE_SLAB_BYTES scratch slab)

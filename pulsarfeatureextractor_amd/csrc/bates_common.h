@@ -90,6 +90,10 @@ constexpr int CTR_GDG = 0;  // batch queue of k_gdgb
 constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS state size)
 constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernels (lm_group.h)
 static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
+// fit slots per wave of k_gdg8g: its SIMT phase (lmpar, one slot per lane) is the largest
+// share of the 8-parameter kernel, which runs one wave per SIMD (registers), so 48 slots
+// fill more lanes there; the LDS state (BlmState<8, 48>, 35 KB) still admits 4 waves per CU
+constexpr int GDG8_FPW = 48;
 // work queues of the pooled kernels (BatesArgs::counters)
 constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6,
               CTR_GHISTG = 7, CTR_GFIXG = 8, CTR_WIDE = 9, CTR_WIDEQ = 10;

@@ -2251,7 +2251,7 @@ struct Gdg8Prob {
 
 template <int P>
 __global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
-  constexpr int FPW = GLM_FPW;
+  constexpr int FPW = GDG8_FPW;
   // 16 lanes (8 rows each) at 128 bins: 32 lanes measured 7 % slower there
   // (profiles/r02_gdg8_g32_ab.txt); 32 lanes (8 rows each) at 256 bins
   constexpr int G = glm_group_lanes(64 * P);
@@ -2259,7 +2259,7 @@ __global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gdg8Prob<P, FPW, G> prob{a, T, a.gslots};
+  Gdg8Prob<P, FPW, G> prob{a, T, a.gslots * GDG8_FPW / GLM_FPW};
   glm_engine<8, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
