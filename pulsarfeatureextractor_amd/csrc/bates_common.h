@@ -94,6 +94,10 @@ static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
 // share of the 8-parameter kernel, which runs one wave per SIMD (registers), so 48 slots
 // fill more lanes there; the LDS state (BlmState<8, 48>, 35 KB) still admits 4 waves per CU
 constexpr int GDG8_FPW = 48;
+// fit slots per wave of the 4-parameter pooled kernels k_gt1g / k_gdgg up to 128 bins (two
+// waves per SIMD: BlmState<4, 44> + slot table + peel rows = 19 KB, 8 waves = 153 KB of LDS
+// per CU; their SIMT phase also runs one slot per lane)
+constexpr int GLM4_FPW = 44;
 // work queues of the pooled kernels (BatesArgs::counters)
 constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6,
               CTR_GHISTG = 7, CTR_GFIXG = 8, CTR_WIDE = 9, CTR_WIDEQ = 10;
@@ -106,7 +110,7 @@ __host__ __device__ constexpr int profile_mpl(int lp) {
 }
 // per-wave scratch of k_gdgb: x and y of FPW fits, 64*MPL rows each
 __host__ __device__ constexpr size_t gdg_wave_scratch_doubles(int lp) {
-  return (size_t)BLM_FPW * 64 * profile_mpl(lp) * 2;
+  return (size_t)(GLM4_FPW > BLM_FPW ? GLM4_FPW : BLM_FPW) * 64 * profile_mpl(lp) * 2;
 }
 
 // persistent waves of a pooled kernel without per-wave scratch that holds `per_simd` waves

@@ -2059,13 +2059,13 @@ struct Gt1Prob {
 
 template <int P>
 __global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
-  constexpr int FPW = GLM_FPW;
+  constexpr int FPW = P <= 2 ? GLM4_FPW : GLM_FPW;  // LDS: 256-bin peel rows keep 32
   constexpr int G = glm_group_lanes(64 * P);
   __shared__ BlmState<4, FPW> S;
   __shared__ SlotTab<FPW> T;
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
-  Gt1Prob<P, FPW, G> prob{a, T, a.gslots};
+  Gt1Prob<P, FPW, G> prob{a, T, a.gslots * FPW / GLM_FPW};
   glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
@@ -2179,7 +2179,7 @@ struct PeelProb {
 
 template <int P>
 __global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
-  constexpr int FPW = GLM_FPW;
+  constexpr int FPW = P <= 2 ? GLM4_FPW : GLM_FPW;  // LDS: 256-bin peel rows keep 32
   __shared__ BlmState<4, FPW> S;
   __shared__ SlotTab<FPW> T;
   __shared__ double ys[64 * P];
@@ -2189,7 +2189,7 @@ __global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
   double* xs = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   double* yv = xs + (size_t)FPW * 64 * P;
   constexpr int G = glm_group_lanes(64 * P);
-  PeelProb<P, FPW, G> prob{a, T, xs, yv, ys, cx, a.gslots};
+  PeelProb<P, FPW, G> prob{a, T, xs, yv, ys, cx, a.gslots * FPW / GLM_FPW};
   glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
