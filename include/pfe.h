@@ -64,7 +64,10 @@ extern "C" {
                                         more than 16384 Freedman-Diaconis bins).  Unreachable
                                         for byte (PHCX) profiles of up to 32768 bins: their
                                         non-zero IQR is a multiple of 0.25, so the bin count
-                                        is at most 510 n^(1/3).  The row is not scored */
+                                        is at most 510 n^(1/3); or, in pfe_bates22, a
+                                        sub-band shape outside nsub 2-256, nBins 1-1024,
+                                        nsub*(nBins+1) <= 32768 -- the other groups' scores
+                                        are still computed).  The row is not scored */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu

@@ -79,6 +79,25 @@ int pfe_phcx_pack(const pfe_phcx_batch* b, const int64_t* rows, int64_t nrows,
                   int64_t dm_stride, uint8_t* sub, int64_t sub_stride, double* dmcurve,
                   int64_t dmc_stride, double* scal);
 void pfe_phcx_free(pfe_phcx_batch* b);
+/* Every file's info in one call: out[0 .. count) (capacity >= pfe_phcx_count(b), else
+   PFE_EINVAL).  Replaces a per-file pfe_phcx_info_get loop on the batched product path. */
+int pfe_phcx_info_all(const pfe_phcx_batch* b, pfe_phcx_info* out, int64_t capacity);
+
+/* Score rows as text, the way DataProcessor writes them:
+     style 0  storeScore      (DataProcessor.py:321-325)  "<name>,v1,...,vw\n"
+     style 1  storeScoreARFF  (DataProcessor.py:421-425)  "v1,...,vw,?%<name>\n"
+     style 2  outputScores    (DataProcessor.py:443-446)  "v1,...,vw\n" (name unused)
+   Every value is Python 2.7's str(float): '%.12g', ".0" appended when the text has no '.',
+   'e' or 'n'; NaN -> "nan", +-inf -> "inf" / "-inf"; then, as the reference does on the
+   joined line, every "nan" and afterwards every "inf" becomes "0" (in the name too).
+   names: the n names back to back in `name_blob`, name i = [name_off[i], name_off[i+1]).
+   vals: row i at vals + i*stride (width doubles).  Rows with skip[i] != 0 are left out
+   (skip may be NULL).  The text goes to buf (capacity cap); *len receives its length.
+   PFE_EINVAL if it does not fit (cap >= sum(name lengths) + n*(24*width + 8) always does). */
+int pfe_format_rows(const char* name_blob, const int64_t* name_off, const double* vals,
+                    int64_t n, int32_t width, int64_t stride, int32_t style,
+                    const uint8_t* skip, int32_t nthreads, char* buf, int64_t cap,
+                    int64_t* len);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,8 @@ EXPORTED_IO_SYMBOLS = (
     "pfe_phcx_fetch",
     "pfe_phcx_pack",
     "pfe_phcx_free",
+    "pfe_phcx_info_all",
+    "pfe_format_rows",
 )
 PFE_PHCX_PROFILE, PFE_PHCX_LYON_DM, PFE_PHCX_SUBBANDS, PFE_PHCX_DM_CURVE, PFE_PHCX_FIT_BLOCK = range(5)
 PFE_IO_STATUS = {0: "ok", 1: "open", 2: "gzip", 3: "xml", 4: "value", 5: "range", 6: "shape"}
@@ -120,6 +122,14 @@ class PhcxInfo(C.Structure):
         ("scal", C.c_double * 8),
     ]
 
+
+# numpy view of pfe_phcx_info (include/pfe_io.h), for pfe_phcx_info_all
+PHCX_INFO_DTYPE = np.dtype([
+    ("status", "<i4"), ("superb", "<i4"), ("section", "<i4"), ("lp", "<i4"),
+    ("nsub", "<i4"), ("lsb", "<i4"), ("ndm", "<i4"), ("reserved", "<i4"),
+    ("ld", "<i8"), ("lfit", "<i8"), ("scal", "<f8", (8,)),
+])
+assert PHCX_INFO_DTYPE.itemsize == C.sizeof(PhcxInfo)
 
 _lib = None
 _lock = threading.Lock()
@@ -209,6 +219,11 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_phcx_pack.argtypes = [vp, vp, i64, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp]
         lib.pfe_phcx_free.restype = None
         lib.pfe_phcx_free.argtypes = [vp]
+        lib.pfe_phcx_info_all.restype = C.c_int
+        lib.pfe_phcx_info_all.argtypes = [vp, vp, i64]
+        lib.pfe_format_rows.restype = C.c_int
+        lib.pfe_format_rows.argtypes = [vp, vp, vp, i64, i32, i64, i32, vp, i32, vp, i64,
+                                        C.POINTER(i64)]
         if path is None:
             _lib = lib
         return lib
@@ -632,26 +647,38 @@ class PhcxBatch:
             raise IndexError(i)
         return inf
 
+    def infos(self) -> np.ndarray:
+        """Every file's pfe_phcx_info as one structured array (PHCX_INFO_DTYPE)."""
+        out = np.empty(len(self.paths), dtype=PHCX_INFO_DTYPE)
+        if self.lib.pfe_phcx_info_all(self._h, out.ctypes.data if len(out) else None,
+                                      len(out)) != PFE_OK:
+            raise PfeError("pfe_phcx_info_all failed")
+        return out
+
     def fetch(self, i: int, field: int, count: int, dtype=np.uint8) -> np.ndarray:
         out = np.empty(count, dtype=dtype)
         if self.lib.pfe_phcx_fetch(self._h, i, field, out.ctypes.data, count) != PFE_OK:
             raise PfeError(f"pfe_phcx_fetch({i}, {field}) failed")
         return out
 
-    def pack(self, rows, lp=None, ld=None, nsub_lsb=None, ndm=None, threads: int = 0):
-        """Dense arrays of the given rows (all of one shape): dict of numpy arrays."""
+    def pack(self, rows, lp=None, ld=None, nsub_lsb=None, ndm=None, threads: int = 0,
+             alloc=None):
+        """Dense arrays of the given rows (all of one shape): dict of numpy arrays.
+        alloc(name, shape, dtype) -> array supplies the destination buffers (e.g. views of
+        reused pinned slabs); default np.empty."""
+        alloc = alloc or (lambda _k, shape, dt: np.empty(shape, dtype=dt))
         rows = np.ascontiguousarray(rows, dtype=np.int64)
         n = len(rows)
-        out = {"scal": np.empty((n, 8), dtype=np.float64)}
+        out = {"scal": alloc("scal", (n, 8), np.float64)}
         ptr = {}
         if lp is not None:
-            out["prof"] = np.empty((n, lp), dtype=np.uint8)
+            out["prof"] = alloc("prof", (n, lp), np.uint8)
         if ld is not None:
-            out["lyon_dm"] = np.empty((n, ld), dtype=np.uint8)
+            out["lyon_dm"] = alloc("lyon_dm", (n, ld), np.uint8)
         if nsub_lsb is not None:
-            out["sub"] = np.empty((n,) + tuple(nsub_lsb), dtype=np.uint8)
+            out["sub"] = alloc("sub", (n,) + tuple(nsub_lsb), np.uint8)
         if ndm is not None:
-            out["dmcurve"] = np.empty((n, ndm), dtype=np.float64)
+            out["dmcurve"] = alloc("dmcurve", (n, ndm), np.float64)
         for k in ("prof", "lyon_dm", "sub", "dmcurve"):
             ptr[k] = out[k].ctypes.data if k in out else None
         rc = self.lib.pfe_phcx_pack(
@@ -662,3 +689,37 @@ class PhcxBatch:
         if rc != PFE_OK:
             raise PfeError("pfe_phcx_pack: rows of another shape or failed files")
         return out
+
+
+def format_rows(names, vals: np.ndarray, style: int = 0, skip=None, threads: int = 0) -> bytes:
+    """pfe_format_rows: the text DataProcessor writes for score rows (storeScore style 0,
+    storeScoreARFF style 1, outputScores style 2) -- see include/pfe_io.h.  names: str or
+    bytes per row; vals (n, width) float64 with contiguous rows; skip: rows to leave out."""
+    lib = load_library()
+    vals = np.asarray(vals, dtype=np.float64)
+    if vals.ndim != 2 or (vals.shape[0] and vals.strides[1] != 8):
+        vals = np.ascontiguousarray(vals.reshape(len(vals), -1))
+    n, width = vals.shape
+    if n == 0:
+        return b""
+    enc = [os.fsencode(x) if isinstance(x, str) else bytes(x) for x in names]
+    if len(enc) != n:
+        raise ValueError("one name per row")
+    blob = b"".join(enc)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum([len(e) for e in enc], out=off[1:])
+    sk = None
+    if skip is not None:
+        sk = np.ascontiguousarray(skip, dtype=np.uint8)
+        if sk.shape != (n,):
+            raise ValueError("skip must have one entry per row")
+    cap = len(blob) + n * (24 * width + 8) + 16
+    buf = C.create_string_buffer(cap)
+    used = C.c_int64()
+    rc = lib.pfe_format_rows(blob, off.ctypes.data, vals.ctypes.data, n, width,
+                             vals.strides[0] // 8, int(style),
+                             None if sk is None else sk.ctypes.data, int(threads), buf, cap,
+                             C.byref(used))
+    if rc != PFE_OK:
+        raise PfeError("pfe_format_rows failed")
+    return buf.raw[:used.value]

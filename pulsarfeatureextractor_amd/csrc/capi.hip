@@ -470,8 +470,14 @@ static int check_bates_in(pfe_handle* h, const pfe_bates_in* in, const char* fn,
     return set_err(h, PFE_EINVAL, "%s: null input array", fn);
   if (in->lp < 8 || in->lp > 1024)
     return set_err(h, PFE_EINVAL, "%s: lp=%d outside [8,1024]", fn, in->lp);
-  if (const char* why = pfe::subband_shape_error(in->nsub, in->lsb))
-    return set_err(h, PFE_EINVAL, "%s: sub-band shape %dx%d: %s", fn, in->nsub, in->lsb, why);
+  // pfe_subband3 computes nothing else, so an unsupported sub-band shape fails the call; in
+  // pfe_bates22 it only fails the rows' sub-band group (PFE_ST_UNSUPPORTED per row)
+  if (!need_dm) {
+    if (const char* why = pfe::subband_shape_error(in->nsub, in->lsb))
+      return set_err(h, PFE_EINVAL, "%s: sub-band shape %dx%d: %s", fn, in->nsub, in->lsb, why);
+  } else if (in->nsub < 1 || in->lsb < 1 || (int64_t)in->nsub * in->lsb > (1 << 24)) {
+    return set_err(h, PFE_EINVAL, "%s: sub-band shape %dx%d", fn, in->nsub, in->lsb);
+  }
   if (need_dm && (in->ndm < 3 || in->ndm > 1024))
     return set_err(h, PFE_EINVAL, "%s: ndm=%d outside [3,1024]", fn, in->ndm);
   return PFE_OK;

@@ -590,6 +590,45 @@ void parallel_for(int64_t n, int nthreads, F&& fn) {
   for (auto& t : th) t.join();
 }
 
+// ---- score text (pfe_format_rows) ----
+// str.replace(pat, "0"): left to right, non-overlapping, as Python does.
+void replace_with_zero(const std::string& in, const char* pat, std::string& out) {
+  out.clear();
+  size_t i = 0;
+  while (i < in.size()) {
+    if (i + 3 <= in.size() && in[i] == pat[0] && in[i + 1] == pat[1] && in[i + 2] == pat[2]) {
+      out += '0';
+      i += 3;
+    } else {
+      out += in[i++];
+    }
+  }
+}
+
+void append_clean_name(std::string& s, const char* p, size_t n) {
+  thread_local std::string a, b;
+  a.assign(p, n);
+  replace_with_zero(a, "nan", b);
+  replace_with_zero(b, "inf", a);
+  s += a;
+}
+
+// Python 2.7 str(float) ('%.12g' + ".0" for integral text), then the writers' nan/inf -> 0.
+void append_py2_value(std::string& s, double x) {
+  if (std::isnan(x)) {
+    s += '0';
+    return;
+  }
+  if (std::isinf(x)) {
+    s += x > 0 ? "0" : "-0";
+    return;
+  }
+  char tmp[40];
+  const int k = std::snprintf(tmp, sizeof tmp, "%.12g", x);
+  s.append(tmp, (size_t)k);
+  if (!std::memchr(tmp, '.', (size_t)k) && !std::memchr(tmp, 'e', (size_t)k)) s += ".0";
+}
+
 }  // namespace
 
 struct pfe_phcx_batch {
@@ -670,5 +709,65 @@ int pfe_phcx_pack(const pfe_phcx_batch* b, const int64_t* rows, int64_t nrows, i
 }
 
 void pfe_phcx_free(pfe_phcx_batch* b) { delete b; }
+
+int pfe_phcx_info_all(const pfe_phcx_batch* b, pfe_phcx_info* out, int64_t capacity) {
+  if (!b || capacity < (int64_t)b->files.size() || (!out && !b->files.empty())) return PFE_EINVAL;
+  for (size_t i = 0; i < b->files.size(); ++i) out[i] = b->files[i].info;
+  return PFE_OK;
+}
+
+int pfe_format_rows(const char* name_blob, const int64_t* name_off, const double* vals,
+                    int64_t n, int32_t width, int64_t stride, int32_t style,
+                    const uint8_t* skip, int32_t nthreads, char* buf, int64_t cap,
+                    int64_t* len) {
+  if (n < 0 || width < 0 || style < 0 || style > 2 || !len || (n > 0 && (!vals || !buf)) ||
+      (style != 2 && n > 0 && (!name_blob || !name_off)) || stride < width)
+    return PFE_EINVAL;
+  *len = 0;
+  if (n == 0) return PFE_OK;
+  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int64_t nt = std::min<int64_t>(nthreads, std::max<int64_t>(1, n / 256));
+  std::vector<std::string> part((size_t)nt);
+  auto work = [&](int64_t t) {
+    const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+    std::string& s = part[(size_t)t];
+    s.reserve((size_t)(r1 - r0) * (size_t)(24 * width + 80));
+    for (int64_t r = r0; r < r1; ++r) {
+      if (skip && skip[r]) continue;
+      if (style == 0) {
+        append_clean_name(s, name_blob + name_off[r], (size_t)(name_off[r + 1] - name_off[r]));
+        s += ',';
+      }
+      const double* v = vals + r * stride;
+      for (int32_t k = 0; k < width; ++k) {
+        if (k) s += ',';
+        append_py2_value(s, v[k]);
+      }
+      if (style == 1) {
+        s += ",?%";
+        append_clean_name(s, name_blob + name_off[r], (size_t)(name_off[r + 1] - name_off[r]));
+      }
+      s += '\n';
+    }
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt);
+    for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& t : th) t.join();
+  }
+  int64_t total = 0;
+  for (const auto& s : part) total += (int64_t)s.size();
+  if (total > cap) return PFE_EINVAL;
+  char* p = buf;
+  for (const auto& s : part) {
+    std::memcpy(p, s.data(), s.size());
+    p += s.size();
+  }
+  *len = total;
+  return PFE_OK;
+}
 
 }  // extern "C"

@@ -729,8 +729,21 @@ static hipError_t launch_sub(const SubArgs& s, hipStream_t st) {
   return launch_sl<16, uint32_t>(s, st);
 }
 
-// the 22-score chain: scores 20-22 into columns 19-21 of out (n x 22)
+__global__ void k_mark_unsupported(uint32_t* status, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicOr(&status[i], PFE_ST_UNSUPPORTED);
+}
+
+// the 22-score chain: scores 20-22 into columns 19-21 of out (n x 22).  A sub-band shape
+// the kernels do not hold (subband_shape_error) fails its rows, not the call: the other
+// groups' scores are still computed and every row gets PFE_ST_UNSUPPORTED.
 hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  if (subband_shape_error(a.nsub, a.lsb)) {
+    hipLaunchKernelGGL(k_mark_unsupported, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0,
+                       st, a.status, a.n);
+    return hipGetLastError();
+  }
   SubArgs s{a.prof, a.lp, a.sub, a.nsub, a.lsb, a.scal, a.n, a.out + 19, 22, a.status};
   return launch_sub(s, st);
 }

@@ -243,15 +243,100 @@ def _stream(paths, parse, score, emit, batch=BATCH):
             emit(cuts[k], paths[cuts[k]:cuts[k + 1]], score(parsed))
 
 
-class DataProcessor:
-    """Same entry points and output semantics as DataProcessor.py, batched on the GPU."""
+class PinnedSlabs:
+    """Pinned host buffers (pfe_host_alloc) reused across batches and grown on demand: the
+    native packer writes each shape group's rows straight into them and libpfe DMAs them in
+    place.  view(key, shape, dtype) -> a numpy view of the slab `key` (valid until the next
+    view of the same key)."""
 
-    def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH):
+    def __init__(self):
+        self._slabs = {}
+
+    def view(self, key, shape, dtype):
+        from ._native import host_empty
+
+        dt = np.dtype(dtype)
+        shape = tuple(int(v) for v in shape)
+        need = max(1, int(np.prod(shape, dtype=np.int64)) * dt.itemsize)
+        s = self._slabs.get(key)
+        if s is None or s.nbytes < need:
+            s = host_empty((need + need // 4 + 4096,), np.uint8)
+            self._slabs[key] = s
+        return s[:need].view(dt)[: int(np.prod(shape, dtype=np.int64))].reshape(shape)
+
+
+class ParsedBatch:
+    """One streamed batch after the host stage.  PHCX / SUPERB files stay inside the native
+    reader (`nb`, pfe_phcx_parse) with their infos as one structured array; only the files it
+    flags are parsed by the Python parser (`fallback`: {k: (PHCXCandidate | None, error)}, k
+    indexing `px`).  PFD files are read by pfd.read (`rd`)."""
+
+    __slots__ = ("paths", "px", "pf", "nb", "info", "fallback", "rd")
+
+    def close(self):
+        if self.nb is not None:
+            self.nb.close()
+            self.nb = None
+
+
+class BatchScores:
+    """GPU stage output for a batch: `mat` (n, width) float64 when every row of the mode has
+    one width (scores, Lyon features, uniform profiles), else `rows` (a list); `err[i]` is
+    None or the failure text of file i."""
+
+    __slots__ = ("mat", "rows", "err")
+
+    def __init__(self, n, width=None):
+        self.mat = np.full((n, width), np.nan) if width else None
+        self.rows = None if width else [None] * n
+        self.err = [None] * n
+
+    def row(self, i):
+        return self.mat[i] if self.mat is not None else self.rows[i]
+
+
+def _groups(keys: np.ndarray, idx: np.ndarray):
+    """Rows `idx` grouped by equal key rows (first-seen order of np.unique)."""
+    if len(idx) == 0:
+        return []
+    uniq, inv = np.unique(keys, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    order = np.argsort(inv, kind="stable")
+    bounds = np.searchsorted(inv[order], np.arange(len(uniq) + 1))
+    return [(tuple(int(v) for v in uniq[g]), idx[order[bounds[g]:bounds[g + 1]]])
+            for g in range(len(uniq))]
+
+
+def default_workers() -> int:
+    """Host threads for the reader: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS when set (the GPU box's per-job CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+class DataProcessor:
+    """Same entry points and output semantics as DataProcessor.py, batched on the GPU.
+
+    start: resume offset -- skip the first `start` discovered candidates (a run that stopped
+    after appending k batches resumes with start = the number of candidates already
+    processed; the reference has no resume and loses the whole run, DataProcessor.py:590-594).
+    """
+
+    def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
+                 start=0, gpu_batch=1 << 18):
         self.debug = debugFlag
         self.engine = engine
-        self.workers = workers
+        self.workers = workers or default_workers()
         self.log = log
         self.batch = batch
+        self.start = int(start)
+        self.gpu_batch = int(gpu_batch)
         self.scoreStore = []
         self.candidateErrorLog = "CandidateErrorLog.txt"
         self.superb = False
@@ -259,6 +344,7 @@ class DataProcessor:
         self.pfd = False
         self.positive = 0
         self.negative = 0
+        self._slabs = PinnedSlabs()
         if not os.path.exists(self.candidateErrorLog):       # :86-87
             writers.append_text(self.candidateErrorLog, "")
 
@@ -267,15 +353,33 @@ class DataProcessor:
         if directory == "":
             directory = os.path.dirname(os.path.realpath(__file__))
         if not single:
-            return discover(directory, regexes)
-        if ".txt" in directory:  # a list of candidate paths (the reference reads self.path)
+            paths = discover(directory, regexes)
+        elif ".txt" in directory:  # a list of candidate paths (the reference reads self.path)
             with open(directory) as f:
-                return [ln.strip() for ln in f if ln.strip()]
-        return [directory]
+                paths = [ln.strip() for ln in f if ln.strip()]
+        else:
+            paths = [directory]
+        if self.start:
+            self.log(f"Resuming after the first {min(self.start, len(paths))} of "
+                     f"{len(paths)} candidates")
+            paths = paths[self.start:]
+        return paths
 
     def _fail(self, cand, why):
         self.log(f"Error reading profile data :\n\t{why}\n{cand}  did not have scores generated.")
         writers.append_text(self.candidateErrorLog, cand + "\n")
+
+    def _fail_batch(self, batch_paths, res):
+        """The reference's per-candidate failure handling (:517-523) for a batch: one log
+        message per failed candidate, one append of their names to the error log."""
+        failed = [i for i, e in enumerate(res.err) if e]
+        for i in failed:
+            self.log(f"Error reading profile data :\n\t{res.err[i]}\n{batch_paths[i]}  "
+                     "did not have scores generated.")
+        if failed:
+            writers.append_text(self.candidateErrorLog,
+                                "".join(batch_paths[i] + "\n" for i in failed))
+        return failed
 
     def _summary(self, processed, ok, failed, start, extra=""):
         end = datetime.datetime.now()
@@ -284,82 +388,181 @@ class DataProcessor:
 
     # ---- parse / score stages ---------------------------------------------------------
     def _parse(self, paths):
-        """Host stage: PHCX / SUPERB files through the native reader (Python parser for the
-        files it flags), PFD files through pfd.read.  -> (px, parsed, pf, read)."""
-        px = [i for i, p in enumerate(paths) if not is_pfd(p)]
-        pf = [i for i, p in enumerate(paths) if is_pfd(p)]
-        parsed = parse_all([paths[i] for i in px], self.workers) if px else []
-        rd = [_read_pfd(paths[i]) for i in pf]
-        return px, parsed, pf, rd
+        """Host stage (helper thread): PHCX / SUPERB files through the native reader's
+        threads (the ctypes call releases the GIL), the Python parser only for files the
+        reader flags; PFD files through pfd.read."""
+        from ._native import PhcxBatch
+
+        pre = ParsedBatch()
+        pre.paths = paths
+        pre.px = np.array([i for i, p in enumerate(paths) if not is_pfd(p)], dtype=np.int64)
+        pre.pf = [i for i, p in enumerate(paths) if is_pfd(p)]
+        pre.nb, pre.info, pre.fallback = None, None, {}
+        if len(pre.px):
+            pre.nb = PhcxBatch([paths[i] for i in pre.px], threads=self.workers)
+            pre.info = pre.nb.infos()
+            for k in np.flatnonzero(pre.info["status"] != 0):
+                pre.fallback[int(k)] = _parse_one(paths[pre.px[k]])
+        pre.rd = [_read_pfd(paths[i]) for i in pre.pf]
+        return pre
+
+    def _eng(self):
+        return self.engine or get_engine()
+
+    def _bates_native(self, pre, mat, err):
+        """22 scores of the reader's good files: one pfe_phcx_pack per (shape, chunk) into
+        pinned slabs, pfe_bates22 on them (DataProcessor.py:491-525 batched)."""
+        from ._native import PfeError
+
+        info, px, sl = pre.info, pre.px, self._slabs
+        ok = np.flatnonzero(info["status"] == 0)
+        keys = np.stack([info["lp"], info["nsub"], info["lsb"], info["ndm"]], 1)[ok]
+        for (lp, nsub, lsb, ndm), rows in _groups(keys, ok):
+            if ndm < 3:  # max() of an empty DM curve / leastsq m < n: the DM fit raises
+                for k in rows:
+                    err[px[k]] = "DM curve fitting exception"
+                continue
+            for s0 in range(0, len(rows), self.gpu_batch):
+                r = rows[s0:s0 + self.gpu_batch]
+                m, dst = len(r), px[r]
+                a = pre.nb.pack(r, lp=lp, nsub_lsb=(nsub, lsb), ndm=ndm, alloc=sl.view,
+                                threads=self.workers)
+                o = sl.view("out22", (m, 22), np.float64)
+                st = sl.view("status", (m,), np.uint32)
+                try:
+                    self._eng().bates22(a["prof"], a["sub"], a["dmcurve"], a["scal"], out=o,
+                                        status=st)
+                except PfeError as e:  # a shape the library refuses fails its rows, not the run
+                    for d in dst:
+                        err[d] = f"Exception: {e}"
+                    continue
+                mat[dst] = o
+                for j in np.flatnonzero(st & 0xFF):
+                    err[dst[j]] = status_error(int(st[j]))
+
+    def _fallback_cands(self, pre, res):
+        """Files the native reader flagged, parsed by the Python parser: (batch indices,
+        PHCXCandidates); their parse errors go straight into res.err."""
+        idx, cands = [], []
+        for k, (c, e) in pre.fallback.items():
+            if c is None:
+                res.err[pre.px[k]] = e
+            else:
+                idx.append(int(pre.px[k]))
+                cands.append(c)
+        return idx, cands
+
+    def _score_phcx(self, pre, mode, res):
+        info, px, sl = pre.info, pre.px, self._slabs
+        ok = np.flatnonzero(info["status"] == 0)
+        fidx, fcands = self._fallback_cands(pre, res)
+        if mode in ("scores", "label"):
+            mat = res.mat if mode == "scores" else np.full((len(pre.paths), 22), np.nan)
+            self._bates_native(pre, mat, res.err)
+            if fcands:
+                sc, errs = score_bates(fcands, self.engine)
+                for j, i in enumerate(fidx):
+                    mat[i], res.err[i] = sc[j], errs[j]
+            if mode == "label":  # Candidate.calculateProfileScores / getDMCurveData
+                from ._native import PFE_PHCX_LYON_DM, PFE_PHCX_PROFILE
+
+                for k in ok:
+                    i = int(px[k])
+                    if res.err[i]:
+                        continue
+                    prof = pre.nb.fetch(int(k), PFE_PHCX_PROFILE, int(info["lp"][k]))
+                    dm = ([] if info["superb"][k] else
+                          list(pre.nb.fetch(int(k), PFE_PHCX_LYON_DM, int(info["ld"][k]))))
+                    res.rows[i] = (mat[i], [float(v) for v in prof], dm)
+                for j, i in enumerate(fidx):
+                    if not res.err[i]:
+                        c = fcands[j]
+                        res.rows[i] = (mat[i], [float(v) for v in c.profile],
+                                       list(c.lyon_dm) if not c.superb else [])
+        elif mode == "lyon8":
+            keys = np.stack([info["lp"], info["ld"]], 1)[ok]
+            for (lp, ld), rows in _groups(keys, ok):
+                for s0 in range(0, len(rows), self.gpu_batch):
+                    r = rows[s0:s0 + self.gpu_batch]
+                    a = pre.nb.pack(r, lp=lp, ld=ld, alloc=sl.view, threads=self.workers)
+                    o = sl.view("out8", (len(r), 8), np.float64)
+                    self._eng().lyon8(a["prof"], a["lyon_dm"], out=o)
+                    res.mat[px[r]] = o
+            if fcands:
+                f = score_lyon8(fcands, self.engine)
+                res.mat[fidx] = f
+        else:  # "profile": the profile bins as float scores (PHCXFile.computeProfileScores)
+            keys = info["lp"][ok][:, None]
+            for (lp,), rows in _groups(keys, ok):
+                a = pre.nb.pack(rows, lp=lp, alloc=sl.view, threads=self.workers)
+                for j, k in enumerate(rows):
+                    res.rows[px[k]] = a["prof"][j].astype(np.float64)
+            for j, i in enumerate(fidx):
+                res.rows[i] = np.asarray(fcands[j].profile, dtype=np.float64)
+
+    def _score_pfd(self, pre, mode, res):
+        pf, rd = pre.pf, pre.rd
+        good = [k for k, (d, e) in enumerate(rd) if d is not None]
+        for k, (d, e) in enumerate(rd):
+            if d is None:
+                res.err[pf[k]] = e
+        datas = [rd[k][0] for k in good]
+        if not datas:
+            return
+        if mode == "profile":       # PFDFile.computeProfileScores (:479-492)
+            _f, profiles, _e = score_pfd(datas, self.engine)
+            for j, k in enumerate(good):
+                res.rows[pf[k]] = np.asarray(profiles[j], dtype=np.float64)
+        elif mode == "lyon8":
+            feats, _prof, errs = score_pfd(datas, self.engine)
+            for j, k in enumerate(good):
+                res.mat[pf[k]], res.err[pf[k]] = feats[j], errs[j]
+        else:
+            sc, errs = score_pfd22(datas, self.engine)
+            if mode == "label":
+                prof, chis, derr = pfd_profile_and_curve(datas, self.engine)
+                for j, k in enumerate(good):
+                    res.err[pf[k]] = errs[j] or derr[j]
+                    res.rows[pf[k]] = (sc[j], [float(v) for v in prof[j]], list(chis[j]))
+            else:
+                for j, k in enumerate(good):
+                    res.mat[pf[k]], res.err[pf[k]] = sc[j], errs[j]
 
     def _score(self, pre, mode):
         """GPU stage.  mode: "scores" (22 scores), "profile" (profile bins), "lyon8" (the 8
-        Lyon features) or "label" ((scores, profile, DM-curve data)).
-        -> {batch index: (row, None) | (None, error)}"""
-        px, parsed, pf, rd = pre
-        res = {}
-        if px:
-            good = [k for k, (c, e) in enumerate(parsed) if c is not None]
-            cands = [parsed[k][0] for k in good]
-            errs = [None] * len(cands)
-            if mode == "profile":
-                rows = [[float(v) for v in c.profile] for c in cands]
-            elif mode == "lyon8":
-                f = score_lyon8(cands, self.engine) if cands else np.zeros((0, 8))
-                rows = [f[j] for j in range(len(cands))]
-            else:
-                sc, errs = score_bates(cands, self.engine)
-                if mode == "label":  # Candidate.calculateProfileScores / getDMCurveData
-                    rows = [(sc[j], [float(v) for v in c.profile],
-                             list(c.lyon_dm) if not c.superb else [])
-                            for j, c in enumerate(cands)]
-                else:
-                    rows = [sc[j] for j in range(len(cands))]
-            for j, k in enumerate(good):
-                res[px[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
-            for k, (c, e) in enumerate(parsed):
-                if c is None:
-                    res[px[k]] = (None, e)
-        if pf:
-            good = [k for k, (d, e) in enumerate(rd) if d is not None]
-            datas = [rd[k][0] for k in good]
-            if mode == "profile":       # PFDFile.computeProfileScores (:479-492)
-                _f, profiles, _e = score_pfd(datas, self.engine)
-                rows = [[float(v) for v in pr] for pr in profiles]
-                errs = [None] * len(datas)
-            elif mode == "lyon8":
-                feats, _prof, errs = score_pfd(datas, self.engine)
-                rows = [feats[j] for j in range(len(datas))]
-            else:
-                sc, errs = score_pfd22(datas, self.engine)
-                if mode == "label":
-                    prof, chis, derr = pfd_profile_and_curve(datas, self.engine)
-                    rows = [(sc[j], [float(v) for v in prof[j]], list(chis[j]))
-                            for j in range(len(datas))]
-                    errs = [e or de for e, de in zip(errs, derr)]
-                else:
-                    rows = [sc[j] for j in range(len(datas))]
-            for j, k in enumerate(good):
-                res[pf[k]] = (None, errs[j]) if errs[j] else (rows[j], None)
-            for k, (d, e) in enumerate(rd):
-                if d is None:
-                    res[pf[k]] = (None, e)
+        Lyon features) or "label" ((scores, profile, DM-curve data)) -> BatchScores."""
+        width = {"scores": 22, "lyon8": 8}.get(mode)
+        res = BatchScores(len(pre.paths), width)
+        try:
+            if len(pre.px):
+                self._score_phcx(pre, mode, res)
+            if pre.pf:
+                self._score_pfd(pre, mode, res)
+        finally:
+            pre.close()
         return res
 
-    def _run(self, paths, mode, on_row):
-        """Stream the paths through parse -> score; on_row(path, row) for every scored
-        candidate (in discovery order), the reference's failure handling for the rest."""
+    def _stream_text(self, paths, mode, out_path, style):
+        """Collective modes: stream parse -> score, append each batch's lines (pfe_format_rows,
+        storeScore / storeScoreARFF text) in discovery order, log failures."""
+        from ._native import format_rows
+
         counts = {"ok": 0, "failed": 0}
 
         def emit(_off, batch_paths, res):
-            for i, p in enumerate(batch_paths):
-                row, err = res[i]
-                if row is None:
-                    self._fail(p, err)
-                    counts["failed"] += 1
-                else:
-                    on_row(p, row)
-                    counts["ok"] += 1
+            failed = self._fail_batch(batch_paths, res)
+            counts["failed"] += len(failed)
+            counts["ok"] += len(batch_paths) - len(failed)
+            mat, skip = _as_matrix(res)
+            if mat is not None:
+                text = format_rows(batch_paths, mat, style, skip, threads=self.workers)
+            else:  # rows of different widths (profile mode over mixed shapes)
+                fmt = writers.arff_line if style == 1 else writers.score_line
+                text = "".join(fmt(p, res.rows[i]) + "\n" for i, p in enumerate(batch_paths)
+                               if not res.err[i]).encode()
+            if text:
+                with open(out_path, "ab") as f:
+                    f.write(text)
 
         _stream(paths, self._parse, lambda pre: self._score(pre, mode), emit, self.batch)
         return counts["ok"], counts["failed"]
@@ -376,32 +579,9 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        pending = []
-
-        def on_row(p, s):
-            pending.append(writers.arff_line(p, s) if arff else writers.score_line(p, s))
-
-        def flush():
-            if pending:
-                writers.append_text(outPath, "".join(x + "\n" for x in pending))
-                pending.clear()
-
-        counts = {"ok": 0, "failed": 0}
-
-        def emit(_off, batch_paths, res):
-            for i, p in enumerate(batch_paths):
-                row, err = res[i]
-                if row is None:
-                    self._fail(p, err)
-                    counts["failed"] += 1
-                else:
-                    on_row(p, row)
-                    counts["ok"] += 1
-            flush()  # append this batch's lines now (bounded memory, partial output survives)
-
         mode = "profile" if genProfileData else "scores"
-        _stream(paths, self._parse, lambda pre: self._score(pre, mode), emit, self.batch)
-        self._summary(len(paths), counts["ok"], counts["failed"], start)
+        ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0)
+        self._summary(len(paths), ok, failed, start)
 
     def processPFDCollectively(self, directory, verbose, outPath, arff, genProfileData,
                                processSingleCandidate):
@@ -426,12 +606,26 @@ class DataProcessor:
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
 
-        def on_row(p, s):
-            with open(p + ".dat", "w") as f:                   # outputScores :429-447
-                f.write(writers.dat_text(s))
+        from ._native import format_rows
 
-        ok, failed = self._run(paths, "scores", on_row)
-        self._summary(len(paths), ok, failed, start)
+        counts = {"ok": 0, "failed": 0}
+
+        def emit(_off, batch_paths, res):
+            failed = self._fail_batch(batch_paths, res)
+            counts["failed"] += len(failed)
+            counts["ok"] += len(batch_paths) - len(failed)
+            mat, skip = _as_matrix(res)
+            keep = [i for i in range(len(batch_paths)) if not res.err[i]]
+            if mat is not None:
+                texts = format_rows(batch_paths, mat, 2, skip).decode().split("\n")
+            else:
+                texts = [writers.dat_text(res.rows[i]) for i in keep]
+            for i, t in zip(keep, texts):
+                with open(batch_paths[i] + ".dat", "w") as f:   # outputScores :429-447
+                    f.write(t)
+
+        _stream(paths, self._parse, lambda pre: self._score(pre, "scores"), emit, self.batch)
+        self._summary(len(paths), counts["ok"], counts["failed"], start)
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
         self.phcx = True
@@ -443,24 +637,8 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
         paths = self._candidates(directory, regexes, single)
-        pending = []
-        counts = {"ok": 0, "failed": 0}
-
-        def emit(_off, batch_paths, res):
-            for i, p in enumerate(batch_paths):
-                row, err = res[i]
-                if row is None:
-                    self._fail(p, err)
-                    counts["failed"] += 1
-                    continue
-                pending.append(writers.arff_line(p, row) if arff else writers.score_line(p, row))
-                counts["ok"] += 1
-            if pending:
-                writers.append_text(outPath, "".join(x + "\n" for x in pending))
-                pending.clear()
-
-        _stream(paths, self._parse, lambda pre: self._score(pre, "lyon8"), emit, self.batch)
-        self._summary(len(paths), counts["ok"], counts["failed"], start)
+        ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0)
+        self._summary(len(paths), ok, failed, start)
 
     def dmprofPFD(self, directory, verbose, outPath, arff, processSingleCandidate):
         self.pfd = True
@@ -517,13 +695,11 @@ class DataProcessor:
         counts = {"ok": 0, "failed": 0}
 
         def emit(_off, batch_paths, res):
+            failed = self._fail_batch(batch_paths, res)
+            counts["failed"] += len(failed)
             for i, p in enumerate(batch_paths):
-                row, err = res[i]
-                if row is None:
-                    self._fail(p, err)
-                    counts["failed"] += 1
-                else:
-                    on_row(p, row)
+                if not res.err[i]:
+                    on_row(p, res.rows[i])
                     counts["ok"] += 1
             for k, path in (("scores", files["scores"]), ("profile", files["profile"]),
                             ("dm", files["dm"]), ("meta", meta)):
@@ -545,3 +721,20 @@ class DataProcessor:
         TypeError); the extra ones are optional here and unused, as in the reference."""
         self.pfd = True
         self.label(directory, verbose, list(PFD_RES))
+
+
+def _as_matrix(res):
+    """(matrix, skip mask) for pfe_format_rows, or (None, None) when the rows differ in width."""
+    skip = np.array([1 if e else 0 for e in res.err], dtype=np.uint8)
+    if res.mat is not None:
+        return res.mat, skip
+    rows = [r for r, e in zip(res.rows, res.err) if not e]
+    widths = {len(r) for r in rows}
+    if len(widths) > 1:
+        return None, None
+    w = widths.pop() if widths else 0
+    mat = np.zeros((len(res.rows), w))
+    for i, (r, e) in enumerate(zip(res.rows, res.err)):
+        if not e:
+            mat[i] = r
+    return mat, skip

@@ -11,18 +11,20 @@ from pulsarfeatureextractor_amd import _native
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "pfe.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(pfe_\w+)\s*\(", src, re.M)))
+def header_functions(name="pfe.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|int64_t)\s+(pfe_\w+)\s*\(",
+                                 src, re.M)))
 
 
 def test_header_and_binding_agree():
     assert header_functions() == sorted(_native.EXPORTED_SYMBOLS)
+    assert header_functions("pfe_io.h") == sorted(_native.EXPORTED_IO_SYMBOLS)
 
 
 def test_library_exports_all_symbols():
     lib = _native.load_library()
-    for s in header_functions():
+    for s in header_functions() + header_functions("pfe_io.h"):
         assert hasattr(lib, s), s
     assert lib.pfe_abi_version() == 1
 

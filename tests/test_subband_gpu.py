@@ -153,3 +153,23 @@ def test_nsub32_vs_reference_golden(engine):
     assert (r[:, 0] == 0).all() and (r[:, 2] == 0).all() and (r[:, 1] <= 1e-9).all(), r.max(axis=0)
     out, st = engine.bates22(prof, sub, curve, scal)
     assert np.array_equal((st & 0xFF) == 0, ok)
+
+
+@pytest.mark.parametrize("nsub,lsb", [(32, 1024), (64, 512), (300, 8)])
+def test_unsupported_subband_shape_fails_rows_not_call(engine, nsub, lsb):
+    """A sub-band shape the kernels do not hold (nsub*(lsb+1) > 32768 or nsub > 256) no
+    longer fails the whole pfe_bates22 call: every row gets PFE_ST_UNSUPPORTED and the other
+    score groups are computed exactly as for the same candidates with a supported shape.
+    pfe_subband3 (nothing else to compute) still refuses the call."""
+    from pulsarfeatureextractor_amd._native import PfeError
+
+    b = bates_batch(64, lp=128, nsub=16, lsb=128, seed=77)
+    rng = np.random.default_rng(3)
+    big = rng.integers(0, 256, (64, nsub, lsb), dtype=np.uint8)
+    o, st = engine.bates22(b["prof"], big, b["dmcurve"], b["scal"])
+    ref, rst = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    assert ((st & 0x10) != 0).all()
+    assert np.array_equal(st & ~np.uint32(0x18), rst & ~np.uint32(0x18))
+    assert np.array_equal(o[:, :19], ref[:, :19], equal_nan=True)
+    with pytest.raises(PfeError):
+        engine.subband3(b["prof"], big, b["scal"])

@@ -5,13 +5,16 @@ native parse -> pfe_bates22 / pfe_lyon8 on the GPU -> score text, phase by phase
   python tools/e2e_bench.py --n 4000 [--dir /tmp/pfe_e2e] [--workers 16] [--mode phases|stream]
 
 The synthetic files follow SURVEY.md §8(d) (128-bin profile, 16x128 sub-bands, a
-128 x 128 DataBlock per section).  Writing them is not timed.
+128 x 128 DataBlock per section, i.e. 128 DM trials, so the DmIndex lists 128 DM values as a
+real PHCX file lists one per DataBlock row).  Writing them is not timed.
 
 --mode phases (default): parse everything, then score everything, phase by phase.
---mode stream: the product path, DataProcessor.processPHCXCollectively -- batches of --batch
-files parsed on a helper thread one batch ahead of the GPU scoring, each batch's lines
-appended to the output in discovery order; reports the wall time and the process's peak RSS
-(run it in its own process so the peak is the streamed path's).
+--mode stream: the product path, DataProcessor.processPHCXCollectively (22 scores) and
+dmprofPHCX (8 Lyon features) -- batches of --batch files parsed by the native reader on a
+helper thread one batch ahead of the GPU stage (pfe_phcx_pack into pinned slabs, libpfe on
+them, pfe_format_rows), each batch's lines appended in discovery order; reports the wall
+time, the native reader's own rate on the same files (parse only, and parse + pack) and the
+process's peak RSS (run it in its own process so the peak is the streamed path's).
 """
 import argparse
 import json
@@ -38,7 +41,7 @@ def _write(args):
     s = b["scal"][0]
     p = os.path.join(d, f"cand_{i:06d}.phcx.gz")
     phcx.write(p, profile=b["prof"][0], subbands=b["sub"][0], datablocks=blocks,
-               dm_start=0.0, dm_end=200.0, n_dm_index=len(blocks[1]),
+               dm_start=0.0, dm_end=200.0, n_dm_index=len(blocks[1]) // 128,
                period_s=float(s[0]) / 1000.0, snr=float(s[1]), dm=float(s[2]), width=float(s[3]))
     return p
 
@@ -46,7 +49,7 @@ def _write(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=4000)
-    ap.add_argument("--dir", default="/tmp/pfe_e2e")
+    ap.add_argument("--dir", default="/tmp/pfe_e2e_r3")
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--mode", choices=["phases", "stream"], default="phases")
     ap.add_argument("--batch", type=int, default=8192)
@@ -59,25 +62,49 @@ def main():
     from pulsarfeatureextractor_amd import processor, writers
     from pulsarfeatureextractor_amd.candidate import get_engine
 
-    eng = get_engine(0)
     if args.mode == "stream":
         import resource
         import tempfile
 
-        out = os.path.join(tempfile.mkdtemp(), "scores.csv")
-        dp = processor.DataProcessor(engine=eng, workers=args.workers, log=lambda *a: None,
-                                     batch=args.batch)
+        from pulsarfeatureextractor_amd._native import PhcxBatch
+
+        paths = processor.discover(args.dir, [processor.PHCX_RE])
+        nfiles = len(paths)
+        res = {"mode": "stream", "files": nfiles, "batch": args.batch, "workers": args.workers}
+        # the native reader alone on the same files (page cache warm after the first pass)
+        for rep in range(2):
+            t0 = time.perf_counter()
+            for s0 in range(0, nfiles, args.batch):
+                b = PhcxBatch(paths[s0:s0 + args.batch], threads=args.workers)
+                b.close()
+            res["reader_parse_files_per_s"] = nfiles / (time.perf_counter() - t0)
         t0 = time.perf_counter()
-        dp.processPHCXCollectively(args.dir, False, out, False, False, False)
-        wall = time.perf_counter() - t0
-        with open(out) as f:
-            nlines = sum(1 for _ in f)
-        nfiles = len(processor.discover(args.dir, [processor.PHCX_RE]))
-        print(json.dumps({"mode": "stream", "files": nfiles, "batch": args.batch,
-                          "wall_s": wall, "files_per_s": nfiles / wall, "lines": nlines,
-                          "peak_rss_MB": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024,
-                          "workers": args.workers}))
+        for s0 in range(0, nfiles, args.batch):
+            b = PhcxBatch(paths[s0:s0 + args.batch], threads=args.workers)
+            inf = b.infos()
+            b.pack(np.arange(len(inf)), lp=128, nsub_lsb=(16, 128), ndm=128,
+                   threads=args.workers)
+            b.close()
+        res["reader_parse_pack_files_per_s"] = nfiles / (time.perf_counter() - t0)
+        eng = get_engine(0)
+        for kind in ("scores", "dmprof"):
+            out = os.path.join(tempfile.mkdtemp(), "scores.csv")
+            dp = processor.DataProcessor(engine=eng, workers=args.workers, log=lambda *a: None,
+                                         batch=args.batch)
+            t0 = time.perf_counter()
+            if kind == "scores":
+                dp.processPHCXCollectively(args.dir, False, out, False, False, False)
+            else:
+                dp.dmprofPHCX(args.dir, False, out, False, False)
+            wall = time.perf_counter() - t0
+            with open(out) as f:
+                nlines = sum(1 for _ in f)
+            res[kind] = {"wall_s": wall, "files_per_s": nfiles / wall, "lines": nlines}
+        res["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+        res["frac_of_reader"] = res["scores"]["files_per_s"] / res["reader_parse_files_per_s"]
+        print(json.dumps(res))
         return
+    eng = get_engine(0)
     paths = processor.discover(args.dir, [processor.PHCX_RE])[: args.n]
     res = {"files": len(paths)}
     t0 = time.perf_counter()
