@@ -22,13 +22,22 @@ Besides the contract fields the JSON line carries:
   cpu_baseline : the reference-equivalent per-candidate numpy/scipy loop (oracle.lyon.lyon8,
                  the scalar port of PHCXFile.py:320-379) timed on this host, 1 core, on a
                  bounded sample of the same synthetic rows (rank 0, N=1 only)
-  extra        : (default run, N=1 only; --no-extra skips it) the other BASELINE configs,
-                 each with its own roofline and CPU baseline:
-                   config3 -- pfe_bates22 over 10M resident config-3 candidates
+  extra        : (--no-extra skips it) the other BASELINE configs, each with its own
+                 roofline and CPU baseline:
+                   config5 -- (every N) BASELINE config 5's shard: 10M candidates per GPU,
+                              8 Lyon + 22 Bates features into one (n, 30) matrix, then the
+                              timed RCCL all-gather of the whole matrix over xGMI (N > 1)
+                 and at N = 1:
+                   config3 -- pfe_bates22 over 10M resident config-3 candidates, with the
+                              check that every 16384-row tile of the tiled batch scored
+                              bit-identically to the first
                    config4 -- pfe_subband3 over 1M candidates of 16 x 256 sub-bands
                    config2_e2e -- config 2 end to end from pinned host memory (PCIe H2D of
                                   the rows + kernel + D2H of the features, pipelined), with
                                   the measured H2D bandwidth of the box
+                   lyon8_phcx -- the 8 Lyon features at the real PHCX shape: 128-bin profile
+                                 + the whole 128 x 128 DataBlock as the DM array (16 KiB rows,
+                                 lyon8_u8_long), with its HBM roofline
 """
 from __future__ import annotations
 
@@ -69,6 +78,8 @@ def parse():
     ap.add_argument("--no-cpu-multicore", action="store_true",
                     help="skip the multi-process CPU baseline of the 22-score paths")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra configs (N=1 lyon8)")
+    ap.add_argument("--config5-n", type=int, default=10_000_000,
+                    help="candidates per GPU of the extra config-5 line (BASELINE: 10M)")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL all-gather that reassembles the feature matrix")
     ap.add_argument("--option", action="append", default=[],
@@ -478,6 +489,7 @@ def run_bates22(ctx, args, n, lp, steps, warmup, small_warm=False):
     }
     if small_warm:
         res["warmup_note"] = "untimed warm-up: one pass over the first 1M rows"
+        res["_status"] = status
     return res, out
 
 
@@ -569,6 +581,126 @@ def run_e2e(ctx, args, n, lp, steps=5):
     }
 
 
+def tiles_identical(ctx, out, status, blk=16384):
+    """tile_bates repeats one blk-row block: every tile's scores and status must be the
+    same bits as the first tile's (a work-queue / indexing fault past a few million rows
+    would show here)."""
+    torch = ctx.torch
+    n = out.shape[0]
+    full = (n // blk) * blk
+    ob = out.view(torch.int64)
+    same = True
+    if full >= blk:
+        t = ob[:full].view(-1, blk, out.shape[1])
+        same &= bool((t == t[:1]).all())
+        s = status[:full].view(-1, blk)
+        same &= bool((s == s[:1]).all())
+    if full < n:
+        same &= bool(torch.equal(ob[full:], ob[: n - full]))
+        same &= bool(torch.equal(status[full:], status[: n - full]))
+    return same
+
+
+def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2):
+    """The 8 Lyon features at the real PHCX shape (PHCXOperations.getDMCurveData :528-539:
+    the Lyon DM array is the whole section-0 DataBlock, nDM x 128 bytes)."""
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    torch = ctx.torch
+    prof, dm = lyon_batch_torch(n, lp, ld, seed=20261023 + ctx.rank, device=ctx.dev)
+    out = torch.empty((n, 8), dtype=torch.float64, device=ctx.dev)
+
+    def step():
+        ctx.eng.lyon8(prof, dm, out=out)
+
+    elapsed, kern_ms, kern_max = ctx.time_steps(step, steps, warmup)
+    per_cand = lp + ld + 8 * 8
+    achieved = per_cand * n / (kern_ms * 1e-3) / 1e9
+    del prof, dm, out
+    return {
+        "value": n * ctx.world * steps / elapsed, "unit": "candidates/sec", "steps": steps,
+        "ms_per_step": elapsed * 1e3 / steps,
+        "workload": f"{n} synthetic candidates per GPU: {lp}-bin profile + {ld}-byte DM array "
+                    f"(a whole 128 x 128 PHCX DataBlock), 8 Lyon features (pfe_lyon8_u8)",
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": f"pfe::lyon8_u8_long<{lp}, 128, {ld // (64 * 128)}>",
+                     "algorithmic_bytes_per_candidate": per_cand,
+                     "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max},
+    }
+
+
+def run_config5(ctx, args, n=10_000_000, lp=128):
+    """BASELINE config 5 (80M candidates on 8 GPUs = 10M per GPU): the 8 Lyon + 22 Bates
+    features of the rank's shard into one (n, 30) fp64 matrix (Engine.features30; the
+    reference's 30 values are DataProcessor.py:884-886 + Candidate.py:116-150), one timed
+    step, then (N > 1) the RCCL all-gather that reassembles the whole matrix, timed alone."""
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    torch = ctx.torch
+    bt = tile_bates(ctx, n, lp, 20261018 + ctx.rank)
+    _, dmrows = lyon_batch_torch(n, lp, args.ld, seed=20261020 + ctx.rank, device=ctx.dev)
+    out = torch.empty((n, 30), dtype=torch.float64, device=ctx.dev)
+    m = min(n, 1_000_000)
+
+    def warm():
+        ctx.eng.features30(bt["prof"][:m], dmrows[:m], bt["sub"][:m], bt["dmcurve"][:m],
+                           bt["scal"][:m], out=out[:m])
+
+    def step():
+        ctx.eng.features30(bt["prof"], dmrows, bt["sub"], bt["dmcurve"], bt["scal"], out=out)
+
+    elapsed, kern_ms, kern_max = ctx.time_steps(step, 1, 0, warm)
+    res = {
+        "value": n * ctx.world / elapsed, "unit": "candidates/sec", "scaling": "weak",
+        "n_gpus": ctx.world, "steps": 1, "ms_per_step": elapsed * 1e3,
+        "workload": f"config 5: {n} synthetic candidates per GPU ({n * ctx.world} in all), "
+                    f"{lp}-bin profile + {args.ld}-bin DM array, 16x{lp} sub-bands, 128-point "
+                    f"DM curve: 8 Lyon + 22 Bates features into one (n, 30) fp64 matrix per "
+                    f"rank",
+        "compute_ms_per_rank": kern_ms, "compute_ms_max_over_ranks": kern_max,
+        "roofline": bates_roofline(n, kern_ms, kern_max, "pfe_lyon8_u8 + pfe_bates22, one step"),
+    }
+    del bt, dmrows
+    torch.cuda.empty_cache()
+    if ctx.dist_on:
+        from pulsarfeatureextractor_amd.distributed import gather_rows
+
+        total = n * ctx.world
+        g = gather_rows(out[: 1 << 16], (1 << 16) * ctx.world)  # warm the communicator
+        del g
+        torch.cuda.synchronize()
+        ctx.barrier()
+        g0 = time.perf_counter()
+        full = gather_rows(out, total)
+        torch.cuda.synchronize()
+        ctx.barrier()
+        gs = time.perf_counter() - g0
+        t = torch.tensor([gs], dtype=torch.float64, device=ctx.dev)
+        if ctx.backend == "nccl":
+            ctx.dist.all_reduce(t, op=ctx.dist.ReduceOp.MAX)
+        else:
+            tc = t.cpu()
+            ctx.dist.all_reduce(tc, op=ctx.dist.ReduceOp.MAX)
+            t = tc
+        gs = float(t[0])
+        nbytes = int(full.numel() * 8)
+        same = bool(torch.equal(full[ctx.rank * n:(ctx.rank + 1) * n].view(torch.int64),
+                                out.view(torch.int64)))
+        res["gather"] = {"ms": gs * 1e3, "rows": int(full.shape[0]), "width": int(full.shape[1]),
+                         "matrix_bytes": nbytes,
+                         "bytes_received_per_rank": nbytes * (ctx.world - 1) // ctx.world,
+                         "algbw_GBps": nbytes * (ctx.world - 1) / ctx.world / gs / 1e9,
+                         "own_shard_roundtrip_identical": same,
+                         "collective": f"all_gather_into_tensor over {ctx.backend} (RCCL over "
+                                       f"xGMI when nccl)"}
+        res["value_with_gather"] = total / (elapsed + gs)
+        del full
+    del out
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     lp_default = {"subband": 256}.get(args.path, 128)
@@ -593,13 +725,18 @@ def main():
             omp = cpu_baseline_lyon8_omp(lp, args.ld)
             if omp is not None:
                 result["cpu_baseline_multicore"] = omp
-        if ctx.world == 1 and not args.no_extra:
+        if not args.no_extra:
             extra = {}
-            del out
-            out = None
+            if not args.gather:
+                del out
+                out = None
             torch.cuda.empty_cache()
-            # config 3 at the 10M rows BASELINE names: 2 timed steps of ~16 s
+            extra["config5"] = run_config5(ctx, args, n=args.config5_n)
+            result["extra"] = extra
+        if ctx.world == 1 and not args.no_extra:
+            # config 3 at the 10M rows BASELINE names: 2 timed steps of ~15 s
             r3, o3 = run_bates22(ctx, args, 10_000_000, 128, steps=2, warmup=0, small_warm=True)
+            r3["tiles_identical"] = tiles_identical(ctx, o3, r3.pop("_status"))
             del o3
             torch.cuda.empty_cache()
             if not args.no_cpu_baseline:
@@ -614,7 +751,8 @@ def main():
                 r4["cpu_baseline"] = cpu_baseline_subband(256, 200)
             extra["config4"] = r4
             extra["config2_e2e"] = run_e2e(ctx, args, n, lp)
-            result["extra"] = extra
+            torch.cuda.empty_cache()
+            extra["lyon8_phcx"] = run_lyon8_phcx(ctx, args)
     elif args.path == "bates22":
         result, out = run_bates22(ctx, args, n, lp, args.steps, args.warmup)
         if want_cpu:

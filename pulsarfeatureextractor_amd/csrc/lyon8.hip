@@ -285,6 +285,134 @@ __global__ __launch_bounds__(256) void lyon8_u8_generic(const uint8_t* __restric
   }
 }
 
+// ---- long DM rows: the real PHCX shape -------------------------------------------------
+// PHCX's Lyon DM array is the whole section-0 DataBlock (PHCXOperations.getDMCurveData
+// :528-539): nDM x 128 bytes (15 360 at nDM = 120, 16 384 at 128) next to a 64/128/256-bin
+// profile.  One wave per candidate; lane l owns the contiguous bytes [l*SEG, (l+1)*SEG) of
+// the DM row (SEG = LPL leaves of M bytes), held in registers after one burst of loads.
+//   * skew / kurt (and mean): exact integer power sums (v_dot4 / v_dot2 as the fast path),
+//     reduced over the wave, then the exact rational moments (128-bit numerators).
+//   * std: numpy's own arithmetic, so it is bit-identical to numpy.std of the row: mean =
+//     the exact sum / n correctly rounded (numpy's float64 sum of bytes is exact), then
+//     d = x - mean and d*d rounded per element and summed in numpy's pairwise order.  For
+//     n = 2^k * M (M a multiple of 8 in (64, 128], k >= 6) numpy's recursion halves down to
+//     2^k leaves of exactly M values with no remainder: each leaf is eight strided running
+//     sums combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), the leaves a perfect binary tree.
+//     Lane l's LPL = 2^(k-6) leaves are the contiguous leaves it holds, combined in-lane as
+//     that tree; the wave's butterfly (wave_sum_f64: xor-1, 2, 4, ... partners, and IEEE
+//     addition is commutative) is exactly the remaining levels of the tree.
+//   * the profile row (LP = 64/128/256 bytes) is read by lanes 0..LP/16-1, 16 B each; its
+//     power sums are exact and LP a power of two, so stats4<LP> is numpy's value bit for bit.
+template <int M>
+__device__ __forceinline__ double leaf_sumsq(const uint8_t* b, double mean) {
+  // b: M bytes of the lane's registers (M % 8 == 0); numpy pairwise_sum leaf (n <= 128)
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const double d = (double)b[j] - mean;
+    r[j] = d * d;
+  }
+#pragma unroll
+  for (int i = 8; i < M; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double d = (double)b[i + j] - mean;
+      r[j] += d * d;
+    }
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+template <int LP, int M, int LPL>
+__global__ __launch_bounds__(256) void lyon8_u8_long(const uint8_t* __restrict__ prof,
+                                                     int64_t ps,
+                                                     const uint8_t* __restrict__ dm,
+                                                     int64_t ds, int64_t n,
+                                                     double* __restrict__ out) {
+  static_assert(M % 8 == 0 && M > 64 && M <= 128, "leaf length");
+  constexpr int SEG = M * LPL;                // bytes per lane
+  constexpr int VEC = (SEG % 16 == 0) ? 16 : 8;
+  constexpr int NV = SEG / VEC;
+  constexpr int LD = 64 * SEG;
+  constexpr int PL = LP / 16;                 // lanes holding the profile
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c < n; c += nwaves) {
+    // ---- one burst of loads: the lane's DM segment and (lanes < PL) 16 B of profile
+    union {
+      u32x4 v16[SEG / 16 > 0 ? SEG / 16 : 1];
+      uint2 v8[SEG / 8];
+      uint32_t w[SEG / 4];
+      uint8_t b[SEG];
+    } seg;
+    const uint8_t* drow = dm + c * ds + lane * SEG;
+    if constexpr (VEC == 16) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        seg.v16[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(drow) + k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const uint64_t q = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(drow) + k);
+        seg.v8[k] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+      }
+    }
+    const int pl = lane < PL ? lane : 0;
+    const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
+    // ---- exact power sums
+    Acc2 sd = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < SEG / 16; ++k)
+      acc2_x4((u32x4){seg.w[4 * k], seg.w[4 * k + 1], seg.w[4 * k + 2], seg.w[4 * k + 3]}, sd);
+    if constexpr (SEG % 16 != 0) {  // the last 8 bytes
+      uint32_t t = 0;
+      acc2_dword(seg.w[SEG / 4 - 2], sd, t);
+      acc2_dword(seg.w[SEG / 4 - 1], sd, t);
+      sd.t4 += t;
+    }
+    Acc2 sp = {0, 0, 0, 0};
+    if (lane < PL) acc2_x4(pq, sp);
+    const long long S1 = wave_sum_i64((long long)sd.s1);
+    const long long S2 = wave_sum_i64((long long)sd.s2);
+    const long long T3 = wave_sum_i64((long long)sd.t3);
+    const unsigned long long T4 = (unsigned long long)wave_sum_i64((long long)sd.t4);
+    sp.s1 = (uint32_t)wave_sum_i64((long long)sp.s1);
+    sp.s2 = (uint32_t)wave_sum_i64((long long)sp.s2);
+    sp.t3 = (int)wave_sum_i64((long long)sp.t3);
+    sp.t4 = (uint64_t)wave_sum_i64((long long)sp.t4);
+    // ---- numpy's std of the DM row
+    const double mean = (double)S1 / (double)LD;
+    double leaf[LPL];
+#pragma unroll
+    for (int l = 0; l < LPL; ++l) leaf[l] = leaf_sumsq<M>(seg.b + l * M, mean);
+    double ssq;
+    if constexpr (LPL == 1) {
+      ssq = leaf[0];
+    } else if constexpr (LPL == 2) {
+      ssq = leaf[0] + leaf[1];
+    } else {
+      ssq = (leaf[0] + leaf[1]) + (leaf[2] + leaf[3]);
+    }
+    ssq = wave_sum_f64(ssq);
+    // ---- finalise: lanes 0-3 the profile statistics, lanes 4-7 the DM row's
+    if (lane < 8) {
+      double v;
+      if (lane < 4) {
+        double st[4];
+        stats4<LP>(sp, st);
+        v = lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : st[3];
+      } else {
+        const long long T1 = S1 - 128ll * LD;
+        const long long T2 = S2 - 256ll * S1 + 16384ll * LD;
+        const Moments mo = moments_i128(LD, T1, T2, T3, T4);
+        const int k = lane - 4;
+        v = k == 0 ? mean : k == 1 ? sqrt(ssq / (double)LD) : stat_k(mo, k);
+      }
+      __builtin_nontemporal_store(v, out + c * 8 + lane);
+    }
+  }
+}
+
 // ---- fp64 rows (PFD) -------------------------------------------------------------------
 // Two-pass fp64, as numpy/scipy: mean = sum/n; m_k = mean((x-mean)^k) with d^3 = d^2*d and
 // d^4 = (d^2)^2 (scipy.stats._moment exponentiation by squares).  One wave per row.
@@ -342,6 +470,15 @@ static inline int grid_for(int64_t work_waves, int cap) {
   return (int)blocks;
 }
 
+// ld = 64 * LPL * M with a lyon8_u8_long instantiation (M in {120, 128}, LPL in {1, 2, 4}):
+// -> 10 * M + LPL, else 0
+static inline int long_row_shape(int ld) {
+  for (int M : {120, 128})
+    for (int LPL : {1, 2, 4})
+      if (ld == 64 * LPL * M) return 10 * M + LPL;
+  return 0;
+}
+
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
                            const Options& o) {
@@ -371,6 +508,31 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
       PFE_L8U(256);
 #undef PFE_L8U
 #undef PFE_L8
+  } else if (aligned && (lp == 64 || lp == 128 || lp == 256) && long_row_shape(ld) > 0) {
+    // real PHCX shape: short profile + the whole DataBlock (lyon8_u8_long)
+    const int shape = long_row_shape(ld);
+    const int grid = grid_for(n, o.lyon8_blocks);
+#define PFE_LL(LP, M, LPL) \
+  hipLaunchKernelGGL((lyon8_u8_long<LP, M, LPL>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out)
+#define PFE_LLP(M, LPL)      \
+  do {                       \
+    if (lp == 64)            \
+      PFE_LL(64, M, LPL);    \
+    else if (lp == 128)      \
+      PFE_LL(128, M, LPL);   \
+    else                     \
+      PFE_LL(256, M, LPL);   \
+  } while (0)
+    switch (shape) {
+      case 1201: PFE_LLP(120, 1); break;
+      case 1202: PFE_LLP(120, 2); break;
+      case 1204: PFE_LLP(120, 4); break;
+      case 1281: PFE_LLP(128, 1); break;
+      case 1282: PFE_LLP(128, 2); break;
+      default: PFE_LLP(128, 4); break;
+    }
+#undef PFE_LLP
+#undef PFE_LL
   } else {
     const int grid = grid_for(2 * n, o.lyon8_blocks);
     hipLaunchKernelGGL(lyon8_u8_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);

@@ -387,3 +387,5 @@ hipError_t launch_pfd22(PfdArgs pa, double* out, uint32_t* status, void* work, s
 }
 
 }  // namespace pfe
+
+PFE_LM_PROFILE_EXPORT(pfd22)

@@ -49,11 +49,18 @@ def gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
     rows = [shard_bounds(n_total, world, r) for r in range(world)]
     width = max(hi - lo for lo, hi in rows)
-    pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
+    equal = all(hi - lo == width for lo, hi in rows)
+    if equal and local.is_contiguous():
+        pad = local  # equal shards (n_total divisible by world): no padding, no trimming copy
+    else:
+        pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        pad[: local.shape[0]] = local
     buf = torch.empty((world * width,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
     dist.all_gather_into_tensor(buf, pad, group=group)
+    if equal:
+        return buf
     parts = [buf[r * width: r * width + (hi - lo)] for r, (lo, hi) in enumerate(rows)]
     return torch.cat(parts, dim=0)
 

@@ -35,37 +35,62 @@ def bates_inputs(d):
     return d["prof"], d["sub"], curves, scal
 
 
-def oracle_with_floor(prof, sub, curve, scal):
-    """Oracle scores of a fresh batch plus that batch's own chaos data (tools/chaos_rows.py,
-    applied to this batch): every leastsq start point nudged by +-1, +-2 and +4 ulp, and two
-    patterns of +-1 ulp on the residuals.  Returns (scores, status, floor, rmax): floor = the
-    fraction of candidates whose score moves by > 1e-5 / > 1e-3 relative under any of them,
-    rmax (n, 22) = each candidate's largest relative move."""
+_PERTS = (None, 1, -1, 2, -2, 4, "r7", "r11")
+
+
+def _oracle_run(args):
+    """One oracle pass over a batch under perturbation `pert` (None: unperturbed)."""
+    pert, prof, sub, curve, scal = args
     import warnings
 
     import oracle.bates as B
 
-    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "tools"))
-    from chaos_rows import nudger, rel, residual_noise
+    tools = os.path.join(os.path.dirname(GOLDEN), "..", "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    from chaos_rows import nudger, residual_noise
 
     orig = B.leastsq
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        a, sa = B.bates22(prof, sub, curve, scal)
-        oka = (sa & 0xFF) == 0
-        rmax = np.zeros_like(a)
-        try:
-            for pert in (nudger(orig, 1), nudger(orig, -1), nudger(orig, 2), nudger(orig, -2),
-                         nudger(orig, 4), residual_noise(orig, 7), residual_noise(orig, 11)):
-                B.leastsq = pert
-                b, sb = B.bates22(prof, sub, curve, scal)
-                okb = (sb & 0xFF) == 0
-                r = rel(a, b)
-                r[oka != okb] = np.inf
-                r[~oka & ~okb] = 0.0
-                rmax = np.maximum(rmax, r)
-        finally:
-            B.leastsq = orig
+    if pert is not None:
+        B.leastsq = nudger(orig, pert) if isinstance(pert, int) else residual_noise(orig, int(pert[1:]))
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            return B.bates22(prof, sub, curve, scal)
+    finally:
+        B.leastsq = orig
+
+
+def oracle_with_floor(prof, sub, curve, scal, workers=1):
+    """Oracle scores of a fresh batch plus that batch's own chaos data (tools/chaos_rows.py,
+    applied to this batch): every leastsq start point nudged by +-1, +-2 and +4 ulp, and two
+    patterns of +-1 ulp on the residuals.  Returns (scores, status, floor, rmax): floor = the
+    fraction of candidates whose score moves by > 1e-5 / > 1e-3 relative under any of them,
+    rmax (n, 22) = each candidate's largest relative move.  workers > 1: the eight passes run
+    in spawned processes (no state is copied from a parent that holds a GPU context)."""
+    tools = os.path.join(os.path.dirname(GOLDEN), "..", "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    from chaos_rows import rel
+
+    jobs = [(p, prof, sub, curve, scal) for p in _PERTS]
+    if workers > 1:
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+
+        with ProcessPoolExecutor(min(workers, len(jobs)), mp_context=mp.get_context("spawn")) as ex:
+            runs = list(ex.map(_oracle_run, jobs))
+    else:
+        runs = [_oracle_run(j) for j in jobs]
+    a, sa = runs[0]
+    oka = (sa & 0xFF) == 0
+    rmax = np.zeros_like(a)
+    for b, sb in runs[1:]:
+        okb = (sb & 0xFF) == 0
+        r = rel(a, b)
+        r[oka != okb] = np.inf
+        r[~oka & ~okb] = 0.0
+        rmax = np.maximum(rmax, r)
     r = rmax[oka]
     floor = {"moved_1e-5": (r > 1e-5).mean(axis=0).tolist(),
              "moved_1e-3": (r > 1e-3).mean(axis=0).tolist()}

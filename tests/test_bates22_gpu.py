@@ -250,3 +250,39 @@ def test_pooled_tiny_and_empty_batches(engine):
         assert np.array_equal(np.nan_to_num(o, nan=7.0), np.nan_to_num(full[:k], nan=7.0)), k
     o, s = engine.bates22(b["prof"][:0], b["sub"][:0], b["dmcurve"][:0], b["scal"][:0])
     assert o.shape == (0, 22) and s.shape == (0,)
+
+
+def test_config3_full_size_10m(engine):
+    """BASELINE config 3 at the size it names: pfe_bates22 over 10M resident candidates (one
+    16384-candidate synthetic block tiled, as bench.py's extra.config3 does).  Every tile's
+    scores and status must be the bits of the first tile (a work-queue or 32-bit indexing
+    fault past a few million rows would break that), and the first 300 rows must meet the
+    fresh-batch oracle bar."""
+    import torch
+
+    n, blk = 10_000_000, 16384
+    b = bates_batch(blk, seed=20261018)
+    reps = (n + blk - 1) // blk
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         .repeat((reps,) + (1,) * (v.ndim - 1))[:n].contiguous() for k, v in b.items()}
+    out, st = engine.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"])
+    engine.synchronize()
+    del t
+    full = (n // blk) * blk
+    ob = out.view(torch.int64)
+    tiles = ob[:full].view(-1, blk, 22)
+    bad = (tiles != tiles[:1]).any(dim=2).any(dim=1)
+    assert not bool(bad.any()), f"tiles differing from tile 0: {torch.nonzero(bad)[:10].flatten().tolist()}"
+    sv = st[:full].view(-1, blk)
+    assert bool((sv == sv[:1]).all()), "status differs between tiles"
+    assert torch.equal(ob[full:], ob[: n - full]) and torch.equal(st[full:], st[: n - full])
+    k = 300
+    o0, s0 = out[:k].cpu().numpy(), st[:k].cpu().numpy().astype(np.uint32)
+    del out, st, ob, tiles, sv
+    torch.cuda.empty_cache()
+    ref, rst, own, rmax = oracle_with_floor(b["prof"][:k], b["sub"][:k], b["dmcurve"][:k],
+                                            b["scal"][:k], workers=8)
+    gold = FLOOR["bates22_phcx128"]
+    floor = {kk: np.maximum(own[kk], gold[kk]).tolist() for kk in gold if kk.startswith("moved")}
+    check_against(o0, s0, ref, (rst & 0xFF) == 0, "config 3 @10M, tile 0", floor, rmax=rmax,
+                  stable_slack=1)

@@ -91,3 +91,27 @@ def test_large_batch_properties(engine):
     idx = torch.randint(0, tp.shape[0], (2000,), generator=torch.Generator().manual_seed(0))
     sp, sd = tp[idx].cpu().numpy(), td[idx].cpu().numpy()
     check(a[idx].cpu().numpy(), lyon8_batched(sp, sd))
+
+
+@pytest.mark.parametrize("lp,ld", [(128, 15360), (128, 16384), (64, 7680), (256, 8192),
+                                   (128, 30720), (64, 32768)])
+def test_long_dm_rows_vs_oracle(engine, lp, ld):
+    """The real PHCX shape (lyon8_u8_long): a 64-256-bin profile and the whole section-0
+    DataBlock (nDM x 128 bytes).  mean and std bit-exact for both rows -- the DM row's std
+    follows numpy's own two-pass pairwise arithmetic -- skew/kurt within 1e-12."""
+    prof, dm = lyon_batch(300, lp, ld, seed=31 + ld, adversarial=True)
+    got = engine.lyon8(prof, dm)
+    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
+
+
+def test_long_dm_rows_golden_dmplane(engine):
+    """Against the reference's own outputs for 128-bin PHCX files whose section-0 DataBlock
+    is a 120 x 128 period-DM plane (tests/golden/lyon8_phcx128_dmplane.npz)."""
+    from golden_util import load
+
+    d = load("lyon8_phcx128_dmplane")
+    prof = np.ascontiguousarray(d["prof"], dtype=np.uint8)
+    dm = np.ascontiguousarray(d["block0"], dtype=np.uint8)
+    got = engine.lyon8(prof, dm)
+    ok = d["ok"].astype(bool)
+    check(got[ok], d["out"][ok], exact_cols=(0, 1, 4, 5))

@@ -23,6 +23,11 @@ SLOTS = {0: 2, 1: 3, 2: 4, 3: 8}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--path", choices=["bates22", "pfd22"], default="bates22",
+                    help="pfd22: PRESTO folds (bench.py's 16x32x128 block) through "
+                         "pfe_pfd_bates22, the DM fit counted in the pfd22 unit")
+    ap.add_argument("--solver", default=None,
+                    help="handle solver option (batched: per-solve statistics are counted)")
     args = ap.parse_args()
     import torch
 
@@ -31,26 +36,42 @@ def main():
 
     lib = _native.load_library(os.path.join(ROOT, "pulsarfeatureextractor_amd", "lib", "libpfe_lmprof.so"))
     _native._lib = lib  # route the Engine through the instrumented build
-    blk = min(args.n, 16384)  # a synthetic block tiled to n rows (as bench.py --path bates22)
-    base = bates_batch(blk, lp=128, lsb=128, seed=31)
-    reps = (args.n + blk - 1) // blk
-    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in base.items()}
-    t = {k: v.repeat((reps,) + (1,) * (v.dim() - 1))[:args.n].contiguous() for k, v in t.items()}
     eng = _native.Engine(0)
-    out = torch.empty((args.n, 22), dtype=torch.float64, device="cuda")
-    st = torch.empty((args.n,), dtype=torch.int32, device="cuda")
+    if args.solver:
+        eng.set_option("solver", args.solver)
+    tags = ("gauss", "sine_dm_sub") + (("pfd22",) if args.path == "pfd22" else ())
     buf = (C.c_ulonglong * 64)()
-    for tag in ("gauss", "sine_dm_sub"):
+    import time
+    if args.path == "bates22":
+        blk = min(args.n, 16384)  # a synthetic block tiled to n rows (as bench.py --path bates22)
+        base = bates_batch(blk, lp=128, lsb=128, seed=31)
+        reps = (args.n + blk - 1) // blk
+        t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in base.items()}
+        t = {k: v.repeat((reps,) + (1,) * (v.dim() - 1))[:args.n].contiguous() for k, v in t.items()}
+        out = torch.empty((args.n, 22), dtype=torch.float64, device="cuda")
+        st = torch.empty((args.n,), dtype=torch.int32, device="cuda")
+        run = lambda: eng.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"], out, st)  # noqa: E731
+    else:
+        sys.path.insert(0, ROOT)
+        from bench import pfd_block
+        from pulsarfeatureextractor_amd import pfd as _pfd
+
+        profs, subfreqs, pscal = _pfd.batch_inputs(pfd_block(min(args.n, 1024), (16, 32, 128), 20261019))
+        tp, tf, ts = (torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (profs, subfreqs, pscal))
+        out = torch.empty((tp.shape[0], 22), dtype=torch.float64, device="cuda")
+        st = torch.empty((tp.shape[0],), dtype=torch.int32, device="cuda")
+        run = lambda: eng.pfd_bates22(tp, tf, ts, out=out, status=st)  # noqa: E731
+    for tag in tags:
         getattr(lib, f"pfe_lmprof_{tag}")(buf, 1)
     torch.cuda.synchronize()
-    import time
     print(f"lm_profile: inputs ready, n={args.n}", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    eng.bates22(t["prof"], t["sub"], t["dmcurve"], t["scal"], out, st)
+    run()
     torch.cuda.synchronize()
-    print(f"lm_profile: bates22 done in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    res = {"_elapsed_s_instrumented": time.perf_counter() - t0, "_n": args.n}
-    for tag in ("gauss", "sine_dm_sub"):
+    print(f"lm_profile: {args.path} done in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    res = {"_elapsed_s_instrumented": time.perf_counter() - t0, "_n": int(out.shape[0]),
+           "_path": args.path, "_solver": args.solver or "default"}
+    for tag in tags:
         fn = getattr(lib, f"pfe_lmprof_{tag}")
         fn.argtypes = [C.c_void_p, C.c_int]
         assert fn(buf, 0) == 0
