@@ -149,18 +149,22 @@ class PHCXFile(CandidateFileInterface):
         self.scores = [float(v) for v in self.data.profile]
         return self.scores
 
-    def _lyon(self, row):
-        r = np.asarray(row, dtype=np.uint8)[None, :]
-        out = self.engine.lyon8(r, r)
-        return [out[0, 0], out[0, 1], out[0, 2], out[0, 3]]
+    def _lyon8(self):
+        """The 8 Lyon features of this candidate -- profile and section-0 DataBlock -- from
+        one pfe_lyon8_u8 call, kept for the second of the two stat-score calls."""
+        if getattr(self, "_l8", None) is None:
+            p = np.ascontiguousarray(np.asarray(self.data.profile, dtype=np.uint8)[None, :])
+            d = np.ascontiguousarray(np.asarray(self.data.lyon_dm, dtype=np.uint8)[None, :])
+            self._l8 = [float(v) for v in self.engine.lyon8(p, d)[0]]
+        return self._l8
 
     def computeProfileStatScores(self):
         """:320-349 — [mean, std, skew, kurtosis] of the profile."""
-        return self._lyon(self.data.profile)
+        return self._lyon8()[:4]
 
     def computeDMCurveStatScores(self):
         """:351-379 — the same statistics of the section-0 DataBlock."""
-        return self._lyon(self.data.lyon_dm)
+        return self._lyon8()[4:]
 
     def getDMCurveData(self):
         """:306-318 — the decoded section-0 DataBlock."""
@@ -188,8 +192,12 @@ class PFDFile(CandidateFileInterface):
         return _pfd.batch_inputs([self.data])
 
     def _dmprof(self):
-        profs, subfreqs, scal = self._batch()
-        return self.engine.pfd_dmprof(profs, subfreqs, scal)
+        """pfe_pfd_dmprof of this fold (profile, chi^2 curve, Lyon features), launched once
+        and shared by the profile / DM-curve / stat-score calls."""
+        if getattr(self, "_dmp", None) is None:
+            profs, subfreqs, scal = self._batch()
+            self._dmp = self.engine.pfd_dmprof(profs, subfreqs, scal)
+        return self._dmp
 
     def isValid(self):
         return self.data.proflen > 0 and self.data.numchan > 0          # :460-475
@@ -242,11 +250,20 @@ class Candidate:
         self.special = "None"
 
     def _file(self, verbose):
-        if ".pfd" in self.candidateName:
-            return PFDFile(verbose, self.candidateName)
-        if ".gz" in self.candidateName:
-            return PHCXFile(verbose, self.candidateName)
-        return SUPERBPHCXFile(verbose, self.candidateName)
+        """The candidate's file object (Candidate.py:136-150 dispatch), parsed once and kept:
+        the reference re-reads the file for every calculate* call (:218, :278); here
+        calculateProfileStatScores and calculateDMCurveStatScores share one parse and one
+        Lyon-8 launch."""
+        f = getattr(self, "_cand_file", None)
+        if f is None:
+            if ".pfd" in self.candidateName:
+                f = PFDFile(verbose, self.candidateName)
+            elif ".gz" in self.candidateName:
+                f = PHCXFile(verbose, self.candidateName)
+            else:
+                f = SUPERBPHCXFile(verbose, self.candidateName)
+            self._cand_file = f
+        return f
 
     def addScores(self, lineFromFile):
         for s in lineFromFile.split(","):

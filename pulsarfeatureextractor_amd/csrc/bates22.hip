@@ -67,8 +67,13 @@ static size_t hand_bytes(int64_t n, int region, int lp) {
   return (size_t)hand_waves(n, region) * slots * k * glm_group_lanes(lp) * sizeof(double);
 }
 
-// waves of k_ghist_wide (each with a WIDE_SLAB_BYTES scratch slab)
-static int wide_waves(int64_t n) { return (int)(n < 256 ? (n > 0 ? n : 1) : 256); }
+// waves of k_ghist_wide (each with a WIDE_SLAB_BYTES = 720 KB scratch slab): one per 64
+// candidates up to 256, so a small batch does not carry 184 MB of slabs for a queue that is
+// usually empty, and a large one still drains a big queue (low-noise data) in parallel
+static int wide_waves(int64_t n) {
+  const int64_t w = n / 64;
+  return (int)(w < 1 ? 1 : w > 256 ? 256 : w);
+}
 
 // workspace layout: [GaussWS x n][counters][hand-over regions][wide queue][wide slabs]
 // [per-wave scratch]

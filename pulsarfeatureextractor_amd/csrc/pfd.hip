@@ -843,24 +843,14 @@ static size_t pfd4_lds_bytes(int nsub, int L) {
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {
   if (a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4) {
     const size_t lds4 = pfd4_lds_bytes(a.nsub, a.L);
-    static size_t configured4 = 0;
-    if (lds4 > 48 * 1024 && lds4 > configured4) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_pfd_dmprof4,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);
-      if (e != hipSuccess) return e;
-      configured4 = lds4;
-    }
+    hipError_t e = ensure_dyn_lds<k_pfd_dmprof4>(lds4);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pfd_dmprof4, dim3((unsigned)a.n), dim3(256), lds4, st, a);
     return hipGetLastError();
   }
   const size_t lds = pfd_lds_bytes(a.nsub, a.L);
-  static size_t configured = 0;
-  if (lds > 48 * 1024 && lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_pfd_dmprof,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    configured = lds;
-  }
+  hipError_t e = ensure_dyn_lds<k_pfd_dmprof>(lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_pfd_dmprof, dim3((unsigned)a.n), dim3(64), lds, st, a);
   return hipGetLastError();
 }

@@ -8,9 +8,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #define PFE_WAVE 64
 
 namespace pfe {
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for kernel K before a launch with `bytes`
+// of dynamic LDS (> 48 KiB): the attribute is per device, and several handles or host
+// threads may launch at once, so the size already set is tracked per device under a lock.
+template <auto K>
+inline hipError_t ensure_dyn_lds(size_t bytes) {
+  if (bytes <= 48 * 1024) return hipSuccess;
+  static std::mutex mu;
+  static size_t done[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const bool track = dev >= 0 && dev < 64;
+  std::lock_guard<std::mutex> lock(mu);
+  if (track && done[dev] >= bytes) return hipSuccess;
+  e = hipFuncSetAttribute(reinterpret_cast<const void*>(K),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess && track) done[dev] = bytes;
+  return e;
+}
 
 // ---- DPP controls (gfx9 encoding) ----------------------------------------------------
 // quad_perm selectors: ctrl = p0 | p1<<2 | p2<<4 | p3<<6

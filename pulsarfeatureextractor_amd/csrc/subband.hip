@@ -676,13 +676,8 @@ static hipError_t launch_sl(const SubArgs& s, hipStream_t st) {
     hipLaunchKernelGGL((k_subband2<SL, PT, 4>), dim3((unsigned)((s.n + 3) / 4)), dim3(256),
                        wave * 4, st, s);
   } else {
-    static size_t configured = 0;
-    if (wave > 48 * 1024 && wave > configured) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_subband2<SL, PT, 1>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave);
-      if (e != hipSuccess) return e;
-      configured = wave;
-    }
+    hipError_t e = ensure_dyn_lds<k_subband2<SL, PT, 1>>(wave);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_subband2<SL, PT, 1>), dim3((unsigned)s.n), dim3(64), wave, st, s);
   }
   return hipGetLastError();
@@ -695,13 +690,8 @@ static hipError_t launch_fast(const SubArgs& s, hipStream_t st) {
     hipLaunchKernelGGL((k_subband_fast<LSB, 4>), dim3((unsigned)((s.n + 3) / 4)), dim3(256),
                        wave * 4, st, s);
   } else {
-    static size_t configured = 0;
-    if (wave > 48 * 1024 && wave > configured) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_subband_fast<LSB, 1>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave);
-      if (e != hipSuccess) return e;
-      configured = wave;
-    }
+    hipError_t e = ensure_dyn_lds<k_subband_fast<LSB, 1>>(wave);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_subband_fast<LSB, 1>), dim3((unsigned)s.n), dim3(64), wave, st, s);
   }
   return hipGetLastError();

@@ -34,8 +34,12 @@ def py2_str(x) -> str:
 
 def py2_scalar_str(x) -> str:
     """Python-2 str() of a numpy scalar as the label writer meets them: integers as
-    integers (the PHCX DM-curve data, PHCXOperations.getDM_FFT :279-293), float32 with 8
-    significant digits (old numpy's float32 str; the PFD chi^2 curve), float64 as py2_str."""
+    integers (the PHCX DM-curve data, PHCXOperations.getDM_FFT :279-293), float64 as
+    py2_str, float32 (the PFD chi^2 curve, PFDFile.py:393) as the numpy of the reference's
+    Python 2 era formats a float32 scalar's str(): '%.6g' (its FLOATPREC_STR; repr used 8
+    digits) with ".0" appended to integral text.  Parity unpinned: the golden label files
+    were written under Python 3, whose str() of a float32 is the shortest repr, so
+    tests/test_label_gpu.py compares that column to 6 significant digits."""
     import numpy as np
 
     if isinstance(x, (int, np.integer)):
@@ -46,7 +50,7 @@ def py2_scalar_str(x) -> str:
             return "nan"
         if math.isinf(v):
             return "inf" if v > 0 else "-inf"
-        s = "%.8g" % v
+        s = "%.6g" % v
         if "." not in s and "e" not in s:
             s += ".0"
         return s

@@ -6,7 +6,7 @@ Compared per candidate (os.walk order is the filesystem's): the same candidates 
 Cands.meta with label "0" and in every CSV with ",0,%<candidate>"; the same failures in
 CandidateErrorLog.txt; profile bins and PHCX DM-curve data exactly (the reference writes
 them with Python 3's shortest repr here and this build with Python 2's str(), so values are
-compared after parsing: float64 to 1e-11, the float32 PFD curve as float32 to 1e-7).  The
+compared after parsing: float64 to 1e-11, the float32 PFD curve to the 6 significant digits Python 2 prints).  The
 PHCX scores are the engine's own scores of the same candidates written as Python 2 writes
 them, and the columns that are bit-exact against the reference equal the reference's; the
 PFD scores are held to the PFD 22-score bar (tests/test_pfd22_gpu.py)."""
@@ -123,7 +123,8 @@ def test_label_pfd(tmp_path, monkeypatch):
     r, o = norm(parse_csv(str(g["pfd_DMCurve.csv"]), "<DIR>")), norm(parse_csv(got["DMCurve.csv"], base))
     for k in r:
         a, b = np.array(r[k], dtype=np.float32), np.array(o[k], dtype=np.float32)
-        assert np.allclose(a, b, rtol=1e-7, atol=0), k
+        # Python 2's str() of a float32 keeps 6 significant digits (writers.py2_scalar_str)
+        assert np.allclose(a, b, rtol=6e-6, atol=0), k
     r, o = norm(parse_csv(str(g["pfd_Scores.csv"]), "<DIR>")), norm(parse_csv(got["Scores.csv"], base))
     keys = sorted(r)
     ref = np.array([r[k] for k in keys])
