@@ -139,6 +139,8 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
   double qtf[N];
 #pragma unroll
   for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
+  {
+  PFE_LA_CONTRACT
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const double ajj = bcast(fjac[0][j], j);
@@ -155,6 +157,7 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
     }
     if (lane == j) fjac[0][j] = rdiag[j];
     qtf[j] = bcast(wa4[0], j);
+  }
   }
   // R (upper triangle) -> LDS: row i lives in lane i
 #pragma unroll

@@ -135,6 +135,7 @@ __device__ __forceinline__ double gbcast(double v, int j) {
 // Euclidean norm of a group-distributed m-vector (rows outside [0,m) hold 0)
 template <int MPL, int G = GLM_G>
 __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
+  PFE_LA_CONTRACT
   double p = 0.0;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) p += f[k] * f[k];
@@ -145,6 +146,7 @@ __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
 template <int N, int MPL, int G = GLM_G>
 __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
                                         double (&acnorm)[N]) {
+  PFE_LA_CONTRACT
   static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
   const int gl = glane<G>();
   double wa[N];
@@ -345,6 +347,8 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   double qtf[N];
 #pragma unroll
   for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
+  {
+  PFE_LA_CONTRACT
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const double ajj = gbcast<G>(fjac[0][j], j);
@@ -361,6 +365,7 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
     }
     if (gl == j) fjac[0][j] = rdiag[j];
     qtf[j] = gbcast<G>(wa4[0], j);
+  }
   }
 #pragma unroll
   for (int j = 0; j < N; ++j)

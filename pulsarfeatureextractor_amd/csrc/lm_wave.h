@@ -20,6 +20,18 @@
 
 #include "wave.h"
 
+// The solver's own linear algebra (qrfac, Q^T f, lmpar, qrsolv, the norms) is contracted
+// into fused multiply-adds: these sums run in another order than MINPACK's sequential loops
+// anyway (tree sums over the m rows), so their last bits are not the reference's either way,
+// and an FMA shortens the serial dependency chains of qrsolv / lmpar (one slot per lane).
+// The residual models and every bit-exact score keep -ffp-contract=off (numpy evaluates each
+// operation rounded).  -DPFE_LA_NOFMA restores the uncontracted solver (A/B builds).
+#ifdef PFE_LA_NOFMA
+#define PFE_LA_CONTRACT
+#else
+#define PFE_LA_CONTRACT _Pragma("clang fp contract(fast)")
+#endif
+
 namespace pfe {
 
 constexpr double LM_FTOL = 1.49012e-08;
@@ -73,6 +85,7 @@ __device__ __forceinline__ long long lm_clock_p() { return 0; }
 // MINPACK enorm of a replicated n-vector (sequential, with the dwarf/giant scaling)
 template <int N>
 __device__ __forceinline__ double enorm_u(const double (&x)[N]) {
+  PFE_LA_CONTRACT
   const double rdwarf = 3.834e-20, rgiant = 1.304e19;
   double s1 = 0, s2 = 0, s3 = 0, x1max = 0, x3max = 0;
   const double agiant = rgiant / (double)N;
@@ -112,6 +125,7 @@ __device__ __forceinline__ double enorm_u(const double (&x)[N]) {
 // Euclidean norm of a distributed m-vector (rows outside [0,m) must hold 0)
 template <int MPL>
 __device__ __forceinline__ double enorm_w(const double (&f)[MPL]) {
+  PFE_LA_CONTRACT
   double p = 0.0;
 #pragma unroll
   for (int k = 0; k < MPL; ++k) p += f[k] * f[k];
@@ -124,6 +138,7 @@ __device__ __forceinline__ bool row_ge(int lane, int k, int j) { return k > 0 ||
 // ---- qrfac (pivot = true) on the distributed m x N matrix a -------------------------------
 template <int N, int MPL>
 __device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N], double (&acnorm)[N]) {
+  PFE_LA_CONTRACT
   const int lane = lane_id();
   double wa[N];
   {
@@ -230,6 +245,7 @@ template <int N>
 __device__ __forceinline__ void qrsolv(double (&r)[N][N], const int (&ipvt)[N],
                                        const double (&diag)[N], const double (&qtb)[N],
                                        double (&x)[N], double (&sdiag)[N]) {
+  PFE_LA_CONTRACT
   double wa[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -301,6 +317,7 @@ __device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
                                       const double (&diag)[N], const double (&qtb)[N],
                                       double delta, double& par, double (&x)[N],
                                       double (&sdiag)[N]) {
+  PFE_LA_CONTRACT
   double wa1[N], wa2[N];
   int nsing = N;
 #pragma unroll

@@ -288,92 +288,102 @@ __global__ __launch_bounds__(256) void lyon8_u8_generic(const uint8_t* __restric
 // ---- long DM rows: the real PHCX shape -------------------------------------------------
 // PHCX's Lyon DM array is the whole section-0 DataBlock (PHCXOperations.getDMCurveData
 // :528-539): nDM x 128 bytes (15 360 at nDM = 120, 16 384 at 128) next to a 64/128/256-bin
-// profile.  One wave per candidate; lane l owns the contiguous bytes [l*SEG, (l+1)*SEG) of
-// the DM row (SEG = LPL leaves of M bytes), held in registers after one burst of loads.
+// profile.  One wave per candidate.
 //   * skew / kurt (and mean): exact integer power sums (v_dot4 / v_dot2 as the fast path),
 //     reduced over the wave, then the exact rational moments (128-bit numerators).
-//   * std: numpy's own arithmetic, so it is bit-identical to numpy.std of the row: mean =
-//     the exact sum / n correctly rounded (numpy's float64 sum of bytes is exact), then
-//     d = x - mean and d*d rounded per element and summed in numpy's pairwise order.  For
-//     n = 2^k * M (M a multiple of 8 in (64, 128], k >= 6) numpy's recursion halves down to
-//     2^k leaves of exactly M values with no remainder: each leaf is eight strided running
-//     sums combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), the leaves a perfect binary tree.
-//     Lane l's LPL = 2^(k-6) leaves are the contiguous leaves it holds, combined in-lane as
-//     that tree; the wave's butterfly (wave_sum_f64: xor-1, 2, 4, ... partners, and IEEE
-//     addition is commutative) is exactly the remaining levels of the tree.
+//   * std: numpy's own arithmetic, so it is bit-identical to numpy.std of the row.  mean =
+//     the exact sum / n correctly rounded (numpy's float64 sum of bytes is exact); then
+//     d = x - mean and d*d rounded per element, and the squares summed the way numpy's
+//     reduction does it: the array in buffered chunks of 8192 elements, each chunk a
+//     pairwise sum (leaves of <= 128 values as eight strided running sums combined
+//     ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), halves split at a multiple of 8), the chunk sums
+//     added in order to 0.  (Measured: this, not one pairwise tree over the whole row, is
+//     numpy.std's order for a 15 360-element row.)
+//   * Rows whose pairwise trees are perfect -- a chunk of length 2^k * M, M a multiple of 8
+//     in (64, 128] -- are laid out so the wave's butterfly IS the tree: the first chunk's
+//     leaves sit in lanes 0-31, the second's in lanes 32-63 (a row of <= 8192 values is one
+//     chunk whose halves take the two half-waves), leaf i of a half in lane i / L (L = 1 or
+//     2 leaves per lane, combined in-lane), lanes past the last leaf hold 0 (x + 0 = x for the
+//     non-negative sums), and wave_sum_f64 adds lanes as xor-1, 2, 4, ... partners (IEEE
+//     addition is commutative), ending with half-wave 0 + half-wave 1 = chunk 0 + chunk 1.
+//     LongShape (host) decides whether ld qualifies; other lengths take lyon8_u8_generic.
 //   * the profile row (LP = 64/128/256 bytes) is read by lanes 0..LP/16-1, 16 B each; its
 //     power sums are exact and LP a power of two, so stats4<LP> is numpy's value bit for bit.
-template <int M>
-__device__ __forceinline__ double leaf_sumsq(const uint8_t* b, double mean) {
-  // b: M bytes of the lane's registers (M % 8 == 0); numpy pairwise_sum leaf (n <= 128)
+struct LongShape {
+  int ld;         // row length
+  int base[2];    // first byte of each half-wave's part
+  int m[2];       // leaf length (a multiple of 8 in (64, 128])
+  int l[2];       // leaves per lane (1 or 2)
+  int lanes[2];   // lanes of the half holding leaves
+};
+
+// numpy pairwise leaf of the 16 words w (8 bytes each, leaf length 8 * count words; words
+// past it are 0x80 bytes and contribute 0)
+__device__ __forceinline__ double leaf_sumsq(const uint64_t (&w)[16], int nwords, double mean) {
   double r[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const double d = (double)b[j] - mean;
-    r[j] = d * d;
-  }
-#pragma unroll
-  for (int i = 8; i < M; i += 8)
+  for (int k = 0; k < 16; ++k) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const double d = (double)b[i + j] - mean;
-      r[j] += d * d;
+      const double d = (double)(uint32_t)((w[k] >> (8 * j)) & 0xFF) - mean;
+      const double sq = k < nwords ? d * d : 0.0;
+      if (k == 0)
+        r[j] = sq;
+      else
+        r[j] += sq;
     }
+  }
   return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
 
-template <int LP, int M, int LPL>
+template <int LP>
 __global__ __launch_bounds__(256) void lyon8_u8_long(const uint8_t* __restrict__ prof,
                                                      int64_t ps,
                                                      const uint8_t* __restrict__ dm,
                                                      int64_t ds, int64_t n,
-                                                     double* __restrict__ out) {
-  static_assert(M % 8 == 0 && M > 64 && M <= 128, "leaf length");
-  constexpr int SEG = M * LPL;                // bytes per lane
-  constexpr int VEC = (SEG % 16 == 0) ? 16 : 8;
-  constexpr int NV = SEG / VEC;
-  constexpr int LD = 64 * SEG;
-  constexpr int PL = LP / 16;                 // lanes holding the profile
+                                                     double* __restrict__ out, LongShape sh) {
+  constexpr int PL = LP / 16;  // lanes holding the profile
   const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, li = lane & 31;
+  const int M = sh.m[h], L = sh.l[h];
+  const bool has = li < sh.lanes[h];
+  const int off0 = sh.base[h] + li * L * M;
+  const int nw0 = has ? M / 8 : 0;
+  const int nw1 = has && L == 2 ? M / 8 : 0;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t c = wave; c < n; c += nwaves) {
-    // ---- one burst of loads: the lane's DM segment and (lanes < PL) 16 B of profile
-    union {
-      u32x4 v16[SEG / 16 > 0 ? SEG / 16 : 1];
-      uint2 v8[SEG / 8];
-      uint32_t w[SEG / 4];
-      uint8_t b[SEG];
-    } seg;
-    const uint8_t* drow = dm + c * ds + lane * SEG;
-    if constexpr (VEC == 16) {
+    // ---- one burst of loads: the lane's (up to) two leaves, 8 B words, and 16 B of profile
+    const uint8_t* drow = dm + c * ds;
+    uint64_t w0[16], w1[16];
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-        seg.v16[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(drow) + k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const uint64_t q = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(drow) + k);
-        seg.v8[k] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
-      }
+    for (int k = 0; k < 16; ++k) {
+      const int a0 = k < nw0 ? off0 + 8 * k : 0;
+      const int a1 = k < nw1 ? off0 + M + 8 * k : 0;
+      w0[k] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(drow + a0));
+      w1[k] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(drow + a1));
     }
     const int pl = lane < PL ? lane : 0;
     const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
-    // ---- exact power sums
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // words outside the leaves: bytes 0x80, y = 0
+      if (k >= nw0) w0[k] = 0x8080808080808080ull;
+      if (k >= nw1) w1[k] = 0x8080808080808080ull;
+    }
+    // ---- exact power sums (0x80 bytes add 128 / 128^2 to S1 / S2, nothing to T3 / T4)
     Acc2 sd = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < SEG / 16; ++k)
-      acc2_x4((u32x4){seg.w[4 * k], seg.w[4 * k + 1], seg.w[4 * k + 2], seg.w[4 * k + 3]}, sd);
-    if constexpr (SEG % 16 != 0) {  // the last 8 bytes
-      uint32_t t = 0;
-      acc2_dword(seg.w[SEG / 4 - 2], sd, t);
-      acc2_dword(seg.w[SEG / 4 - 1], sd, t);
-      sd.t4 += t;
+    for (int k = 0; k < 16; k += 2) {
+      acc2_x4((u32x4){(uint32_t)w0[k], (uint32_t)(w0[k] >> 32), (uint32_t)w0[k + 1],
+                      (uint32_t)(w0[k + 1] >> 32)}, sd);
+      acc2_x4((u32x4){(uint32_t)w1[k], (uint32_t)(w1[k] >> 32), (uint32_t)w1[k + 1],
+                      (uint32_t)(w1[k + 1] >> 32)}, sd);
     }
+    const int pad = 8 * (32 - nw0 - nw1);  // 0x80 bytes counted above
     Acc2 sp = {0, 0, 0, 0};
     if (lane < PL) acc2_x4(pq, sp);
-    const long long S1 = wave_sum_i64((long long)sd.s1);
-    const long long S2 = wave_sum_i64((long long)sd.s2);
+    const long long S1 = wave_sum_i64((long long)sd.s1 - 128ll * pad);
+    const long long S2 = wave_sum_i64((long long)sd.s2 - 16384ll * pad);
     const long long T3 = wave_sum_i64((long long)sd.t3);
     const unsigned long long T4 = (unsigned long long)wave_sum_i64((long long)sd.t4);
     sp.s1 = (uint32_t)wave_sum_i64((long long)sp.s1);
@@ -381,19 +391,9 @@ __global__ __launch_bounds__(256) void lyon8_u8_long(const uint8_t* __restrict__
     sp.t3 = (int)wave_sum_i64((long long)sp.t3);
     sp.t4 = (uint64_t)wave_sum_i64((long long)sp.t4);
     // ---- numpy's std of the DM row
-    const double mean = (double)S1 / (double)LD;
-    double leaf[LPL];
-#pragma unroll
-    for (int l = 0; l < LPL; ++l) leaf[l] = leaf_sumsq<M>(seg.b + l * M, mean);
-    double ssq;
-    if constexpr (LPL == 1) {
-      ssq = leaf[0];
-    } else if constexpr (LPL == 2) {
-      ssq = leaf[0] + leaf[1];
-    } else {
-      ssq = (leaf[0] + leaf[1]) + (leaf[2] + leaf[3]);
-    }
-    ssq = wave_sum_f64(ssq);
+    const double dn = (double)sh.ld;
+    const double mean = (double)S1 / dn;
+    const double ssq = wave_sum_f64(leaf_sumsq(w0, nw0, mean) + leaf_sumsq(w1, nw1, mean));
     // ---- finalise: lanes 0-3 the profile statistics, lanes 4-7 the DM row's
     if (lane < 8) {
       double v;
@@ -402,11 +402,11 @@ __global__ __launch_bounds__(256) void lyon8_u8_long(const uint8_t* __restrict__
         stats4<LP>(sp, st);
         v = lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : st[3];
       } else {
-        const long long T1 = S1 - 128ll * LD;
-        const long long T2 = S2 - 256ll * S1 + 16384ll * LD;
-        const Moments mo = moments_i128(LD, T1, T2, T3, T4);
+        const long long T1 = S1 - 128ll * sh.ld;
+        const long long T2 = S2 - 256ll * S1 + 16384ll * sh.ld;
+        const Moments mo = moments_i128(sh.ld, T1, T2, T3, T4);
         const int k = lane - 4;
-        v = k == 0 ? mean : k == 1 ? sqrt(ssq / (double)LD) : stat_k(mo, k);
+        v = k == 0 ? mean : k == 1 ? sqrt(ssq / dn) : stat_k(mo, k);
       }
       __builtin_nontemporal_store(v, out + c * 8 + lane);
     }
@@ -470,13 +470,39 @@ static inline int grid_for(int64_t work_waves, int cap) {
   return (int)blocks;
 }
 
-// ld = 64 * LPL * M with a lyon8_u8_long instantiation (M in {120, 128}, LPL in {1, 2, 4}):
-// -> 10 * M + LPL, else 0
-static inline int long_row_shape(int ld) {
-  for (int M : {120, 128})
-    for (int LPL : {1, 2, 4})
-      if (ld == 64 * LPL * M) return 10 * M + LPL;
-  return 0;
+// one chunk of numpy's reduction as a perfect pairwise tree: len = 2^k * m, m a multiple
+// of 8 in (64, 128]; -> (m, leaves) or false
+static bool perfect_chunk(int len, int& m, int& leaves) {
+  leaves = 1;
+  while (len > 128) {
+    if (len % 16) return false;  // halves must stay multiples of 8
+    len /= 2;
+    leaves *= 2;
+  }
+  m = len;
+  return len > 64 && len % 8 == 0;
+}
+
+// place a chunk's (or half-chunk's) leaves on the 32 lanes of half-wave h
+static bool place_half(LongShape& sh, int h, int base, int len) {
+  int m, leaves;
+  if (!perfect_chunk(len, m, leaves) || leaves > 64) return false;
+  sh.base[h] = base;
+  sh.m[h] = m;
+  sh.l[h] = leaves > 32 ? 2 : 1;
+  sh.lanes[h] = leaves > 32 ? 32 : leaves;
+  return true;
+}
+
+// lyon8_u8_long's layout of a DM row of ld bytes (numpy: chunks of 8192, each pairwise)
+static bool long_row_shape(int ld, LongShape& sh) {
+  sh.ld = ld;
+  if (ld <= 256) return false;  // short rows: the fast / generic kernels
+  if (ld <= 8192) {             // one chunk: its two halves take the two half-waves
+    return ld % 16 == 0 && place_half(sh, 0, 0, ld / 2) && place_half(sh, 1, ld / 2, ld / 2);
+  }
+  if (ld <= 16384) return place_half(sh, 0, 0, 8192) && place_half(sh, 1, 8192, ld - 8192);
+  return false;
 }
 
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
@@ -508,31 +534,16 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
       PFE_L8U(256);
 #undef PFE_L8U
 #undef PFE_L8
-  } else if (aligned && (lp == 64 || lp == 128 || lp == 256) && long_row_shape(ld) > 0) {
+  } else if (LongShape sh{}; aligned && (lp == 64 || lp == 128 || lp == 256) &&
+                                long_row_shape(ld, sh)) {
     // real PHCX shape: short profile + the whole DataBlock (lyon8_u8_long)
-    const int shape = long_row_shape(ld);
     const int grid = grid_for(n, o.lyon8_blocks);
-#define PFE_LL(LP, M, LPL) \
-  hipLaunchKernelGGL((lyon8_u8_long<LP, M, LPL>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out)
-#define PFE_LLP(M, LPL)      \
-  do {                       \
-    if (lp == 64)            \
-      PFE_LL(64, M, LPL);    \
-    else if (lp == 128)      \
-      PFE_LL(128, M, LPL);   \
-    else                     \
-      PFE_LL(256, M, LPL);   \
-  } while (0)
-    switch (shape) {
-      case 1201: PFE_LLP(120, 1); break;
-      case 1202: PFE_LLP(120, 2); break;
-      case 1204: PFE_LLP(120, 4); break;
-      case 1281: PFE_LLP(128, 1); break;
-      case 1282: PFE_LLP(128, 2); break;
-      default: PFE_LLP(128, 4); break;
-    }
-#undef PFE_LLP
-#undef PFE_LL
+    if (lp == 64)
+      hipLaunchKernelGGL(lyon8_u8_long<64>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
+    else if (lp == 128)
+      hipLaunchKernelGGL(lyon8_u8_long<128>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
+    else
+      hipLaunchKernelGGL(lyon8_u8_long<256>, dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
   } else {
     const int grid = grid_for(2 * n, o.lyon8_blocks);
     hipLaunchKernelGGL(lyon8_u8_generic, dim3(grid), dim3(256), 0, st, prof, ps, lp, dm, ds, ld, n, out);

@@ -14,6 +14,53 @@ CLASS_E = (2,)                            # s3: integer peak count
 SELF_NOISY = (9, 10)                      # s10, s11: the reference disagrees with itself
 
 
+ENVELOPE_TOL = 1e-5   # the north star's relative bar, applied at both ends of an envelope
+ENVELOPE_TIGHT = 1e-7  # an envelope narrower than this (relative) is a reproducible value
+
+
+def envelope_check(out, st, name, skip=(), cols=slice(None)):
+    """Row-by-row pin of a golden set's LM scores against the reference's own spread
+    (tests/golden/chaos_envelope.npz, tools/chaos_envelope.py: per candidate the min / max
+    over K = 50 samples -- the golden value, the oracle's own run and 48 ulp-scale nudges of
+    start points and residuals).
+
+      * tight rows (the K samples agree to 1e-7): the GPU value must lie inside
+        [lo - 1e-5 |lo|, hi + 1e-5 |hi|] -- every such row, s10/s11 included;
+      * wide rows (the reference itself spreads): the GPU value is one more draw of the same
+        chaotic process and falls outside the K samples' range with probability p = 2/(K+1);
+        the count outside is held to n p + 3 sqrt(n p (1-p)) + 1.
+
+    Rows the reference fails, or whose failure status changes under a nudge, are skipped
+    (the failure pattern itself is checked exactly by the callers).  Returns per-score
+    statistics {score: (tight rows, wide rows, outside wide, bound)}."""
+    env = np.load(os.path.join(GOLDEN, "chaos_envelope.npz"))
+    d = load(name)
+    lo, hi, fixed = env[f"{name}_lo"], env[f"{name}_hi"], env[f"{name}_fixed"]
+    gold = d["out"][:, cols]
+    k = len(env["runs"]) + 1
+    p = 2.0 / (k + 1)
+    ok = d["ok"].astype(bool) & fixed & ((st & 0xFF) == 0)
+    with np.errstate(all="ignore"):
+        inside = (out >= lo - ENVELOPE_TOL * np.abs(lo)) & (out <= hi + ENVELOPE_TOL * np.abs(hi))
+        tight = (hi - lo) <= ENVELOPE_TIGHT * np.maximum(np.abs(lo), np.abs(hi))
+    inside |= (out == gold) | (np.isnan(out) & np.isnan(gold))
+    stats = {}
+    for j in range(22):
+        if j in skip:
+            continue
+        t, w = ok & tight[:, j], ok & ~tight[:, j]
+        bad_t = np.where(t & ~inside[:, j])[0]
+        assert len(bad_t) == 0, (f"{name}: s{j + 1} outside the reference's envelope on "
+                                 f"{len(bad_t)} rows where it is tight (rows {bad_t[:10].tolist()})")
+        nw = int(w.sum())
+        out_w = int((w & ~inside[:, j]).sum())
+        bound = nw * p + 3.0 * np.sqrt(nw * p * (1 - p)) + 1.0
+        assert out_w <= bound, (f"{name}: s{j + 1} outside the reference's envelope on {out_w} "
+                                f"of {nw} chaotic rows (binomial bound {bound:.1f} at p = {p:.3f})")
+        stats[j + 1] = (int(t.sum()), nw, out_w, bound)
+    return stats
+
+
 def load(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 

@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 from golden_util import GOLDEN, bates_inputs, load
-from test_bates22_gpu import check_against
+from golden_util import envelope_check
+from test_bates22_gpu import BITEXACT, check_against
 
 pytestmark = pytest.mark.gpu
 
@@ -38,6 +39,7 @@ def test_features30_vs_reference_golden(engine):
     rmax = np.load(os.path.join(GOLDEN, "chaos_rows.npz"))["all30_phcx128_rmax"]
     check_against(out[:, 8:], st, np.where(ok[:, None], ref[:, 8:], np.nan), ok, "all30", floor,
                   rmax=rmax)
+    envelope_check(out[:, 8:], st, "all30_phcx128", skip=BITEXACT, cols=slice(8, None))
 
 
 def test_features30_device_matches_host(engine):

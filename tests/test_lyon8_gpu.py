@@ -94,14 +94,24 @@ def test_large_batch_properties(engine):
 
 
 @pytest.mark.parametrize("lp,ld", [(128, 15360), (128, 16384), (64, 7680), (256, 8192),
-                                   (128, 30720), (64, 32768)])
+                                   (128, 12800), (128, 8320), (64, 384), (256, 10240)])
 def test_long_dm_rows_vs_oracle(engine, lp, ld):
     """The real PHCX shape (lyon8_u8_long): a 64-256-bin profile and the whole section-0
-    DataBlock (nDM x 128 bytes).  mean and std bit-exact for both rows -- the DM row's std
-    follows numpy's own two-pass pairwise arithmetic -- skew/kurt within 1e-12."""
+    DataBlock (nDM x 128 bytes; nDM = 120, 128, 60, 64, 100, 65, 3, 80).  mean and std
+    bit-exact for both rows -- the DM row's std follows numpy's own reduction (8192-element
+    chunks, each a pairwise tree) -- skew/kurt within 1e-12."""
     prof, dm = lyon_batch(300, lp, ld, seed=31 + ld, adversarial=True)
     got = engine.lyon8(prof, dm)
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
+
+
+@pytest.mark.parametrize("ld", [16256, 4352, 30720])
+def test_long_dm_rows_other_lengths(engine, ld):
+    """DataBlock lengths whose numpy pairwise trees are not perfect (nDM = 127, 34, 240):
+    the generic kernel, exact rational moments -- means bit-exact, the rest within 1e-12."""
+    prof, dm = lyon_batch(200, 128, ld, seed=7 + ld, adversarial=True)
+    got = engine.lyon8(prof, dm)
+    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4))
 
 
 def test_long_dm_rows_golden_dmplane(engine):

@@ -170,6 +170,12 @@ def test_unsupported_subband_shape_fails_rows_not_call(engine, nsub, lsb):
     ref, rst = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     assert ((st & 0x10) != 0).all()
     assert np.array_equal(st & ~np.uint32(0x18), rst & ~np.uint32(0x18))
+    # with the score groups concurrent, a group may skip a row another group has already
+    # failed (its outputs are dropped anyway); in order (serial=1) every group runs fully,
+    # and the other groups' scores are the supported shape's, bit for bit
+    with engine.options(serial=1):
+        o, st = engine.bates22(b["prof"], big, b["dmcurve"], b["scal"])
+    assert ((st & 0x10) != 0).all()
     assert np.array_equal(o[:, :19], ref[:, :19], equal_nan=True)
     with pytest.raises(PfeError):
         engine.subband3(b["prof"], big, b["scal"])
