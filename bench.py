@@ -667,12 +667,15 @@ def run_config5(ctx, args, n=10_000_000, lp=128):
         from pulsarfeatureextractor_amd.distributed import gather_rows
 
         total = n * ctx.world
-        g = gather_rows(out[: 1 << 16], (1 << 16) * ctx.world)  # warm the communicator
+        # RCCL gathers device memory; a gloo rehearsal (PFE_BENCH_BACKEND=gloo, ranks sharing
+        # one GPU) gathers a host copy
+        src = out if ctx.backend == "nccl" else out.cpu()
+        g = gather_rows(src[: 1 << 16], (1 << 16) * ctx.world)  # warm the communicator
         del g
         torch.cuda.synchronize()
         ctx.barrier()
         g0 = time.perf_counter()
-        full = gather_rows(out, total)
+        full = gather_rows(src, total)
         torch.cuda.synchronize()
         ctx.barrier()
         gs = time.perf_counter() - g0
@@ -686,7 +689,7 @@ def run_config5(ctx, args, n=10_000_000, lp=128):
         gs = float(t[0])
         nbytes = int(full.numel() * 8)
         same = bool(torch.equal(full[ctx.rank * n:(ctx.rank + 1) * n].view(torch.int64),
-                                out.view(torch.int64)))
+                                src.view(torch.int64)))
         res["gather"] = {"ms": gs * 1e3, "rows": int(full.shape[0]), "width": int(full.shape[1]),
                          "matrix_bytes": nbytes,
                          "bytes_received_per_rank": nbytes * (ctx.world - 1) // ctx.world,
@@ -695,7 +698,7 @@ def run_config5(ctx, args, n=10_000_000, lp=128):
                          "collective": f"all_gather_into_tensor over {ctx.backend} (RCCL over "
                                        f"xGMI when nccl)"}
         res["value_with_gather"] = total / (elapsed + gs)
-        del full
+        del full, src
     del out
     torch.cuda.empty_cache()
     return res

@@ -229,6 +229,12 @@ def load_library(path: str | None = None) -> C.CDLL:
         return lib
 
 
+def _row_stride(stride, a):
+    """Row stride in elements; a single-row array may carry any stride on its row axis
+    (numpy's and torch's relaxed strides, e.g. x[None, :] has stride 0): use the row length."""
+    return a.shape[1] if a.shape[0] <= 1 else stride
+
+
 def _ptr(a) -> int:
     """Raw address of a numpy array or a torch tensor (host or device)."""
     if isinstance(a, np.ndarray):
@@ -422,7 +428,7 @@ class Engine:
             self._dev(out, "out", (torch.float64,), (n, 8))
             if status is not None:
                 self._status_dev(status, n)
-            ps, ds = prof.stride(0), dm.stride(0)
+            ps, ds = _row_stride(prof.stride(0), prof), _row_stride(dm.stride(0), dm)
             flags = PFE_FLAG_DEVICE_PTRS
         else:
             if prof.dtype == np.uint8 and dm.dtype == np.uint8:
@@ -433,7 +439,8 @@ class Engine:
                 raise TypeError("lyon8: rows must be uint8 or float64 (same dtype)")
             prof = prof if prof.strides[1] == prof.itemsize else np.ascontiguousarray(prof)
             dm = dm if dm.strides[1] == dm.itemsize else np.ascontiguousarray(dm)
-            ps, ds = prof.strides[0] // prof.itemsize, dm.strides[0] // dm.itemsize
+            ps = _row_stride(prof.strides[0] // prof.itemsize, prof)
+            ds = _row_stride(dm.strides[0] // dm.itemsize, dm)
             out = self._out_host(out, n, 8)
             if status is not None:
                 self._status_host(status, n)
@@ -717,7 +724,7 @@ def format_rows(names, vals: np.ndarray, style: int = 0, skip=None, threads: int
     buf = C.create_string_buffer(cap)
     used = C.c_int64()
     rc = lib.pfe_format_rows(blob, off.ctypes.data, vals.ctypes.data, n, width,
-                             vals.strides[0] // 8, int(style),
+                             _row_stride(vals.strides[0] // 8, vals), int(style),
                              None if sk is None else sk.ctypes.data, int(threads), buf, cap,
                              C.byref(used))
     if rc != PFE_OK:

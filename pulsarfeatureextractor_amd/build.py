@@ -16,7 +16,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 BUILDDIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIBDIR, "libpfe.so")
-SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip", "subband.hip",
+SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip", "bates_gauss_peel.hip",
+           "bates_gauss_dg8.hip", "subband.hip",
            "pfd.hip", "pfd22.hip"]
 HOST_SOURCES = ["phcx_io.cpp"]  # host-only C++ (PHCX reader / batch packer), built with g++
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]
@@ -89,7 +90,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
             raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         return r
 
-    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or not os.path.exists(lib):
         tmp = lib + ".tmp"

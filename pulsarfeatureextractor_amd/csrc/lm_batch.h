@@ -103,8 +103,9 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
     x[j] = temp + h;
     fn_eval_col<Fn, N, MPL>(fcn, x, j, wa4, cache);
     x[j] = temp;
+    const double rh = 1.0 / h;
 #pragma unroll
-    for (int k = 0; k < MPL; ++k) fjac[k][j] = (wa4[k] - fvec[k]) / h;
+    for (int k = 0; k < MPL; ++k) fjac[k][j] = la_quot(wa4[k] - fvec[k], h, rh);
   }
   nfev += N;
   int ipvt[N];

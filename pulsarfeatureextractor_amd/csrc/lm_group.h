@@ -203,9 +203,10 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
     double ajnorm = sqrt(gsum<G>(p));
     if (ajnorm != 0.0) {
       if (gbcast<G>(a[0][j], j) < 0.0) ajnorm = -ajnorm;
+      const double rinv = 1.0 / ajnorm;
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
-        if (row_ge(gl, k, j)) a[k][j] = a[k][j] / ajnorm;
+        if (row_ge(gl, k, j)) a[k][j] = la_quot(a[k][j], ajnorm, rinv);
       if (gl == j) a[0][j] = a[0][j] + 1.0;
       double d[N];
 #pragma unroll
@@ -220,9 +221,10 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       }
       gsum_from<N, G>(d, j + 1);
       const double ajj = gbcast<G>(a[0][j], j);
+      const double rajj = 1.0 / ajj;
 #pragma unroll
       for (int c = j + 1; c < N; ++c) {
-        const double temp = d[c] / ajj;
+        const double temp = la_quot(d[c], ajj, rajj);
 #pragma unroll
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
@@ -319,8 +321,9 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
     x[j] = temp + h;
     fn_eval_col<Fn, N, MPL>(fcn, x, j, wa4, cache);
     x[j] = temp;
+    const double rh = 1.0 / h;
 #pragma unroll
-    for (int k = 0; k < MPL; ++k) fjac[k][j] = (wa4[k] - fvec[k]) / h;
+    for (int k = 0; k < MPL; ++k) fjac[k][j] = la_quot(wa4[k] - fvec[k], h, rh);
   }
   nfev += N;
   int ipvt[N];

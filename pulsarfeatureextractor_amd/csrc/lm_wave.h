@@ -26,13 +26,28 @@
 // and an FMA shortens the serial dependency chains of qrsolv / lmpar (one slot per lane).
 // The residual models and every bit-exact score keep -ffp-contract=off (numpy evaluates each
 // operation rounded).  -DPFE_LA_NOFMA restores the uncontracted solver (A/B builds).
+// For the same reason the quotients by one per-column divisor (the forward-difference step h
+// of fdjac2, the Householder norm of qrfac) are products with its reciprocal: one division
+// per column instead of one per row.
 #ifdef PFE_LA_NOFMA
 #define PFE_LA_CONTRACT
+constexpr bool LA_EXACT_QUOTIENTS = true;
 #else
 #define PFE_LA_CONTRACT _Pragma("clang fp contract(fast)")
+constexpr bool LA_EXACT_QUOTIENTS = false;
 #endif
 
 namespace pfe {
+
+// x / d of the solver's linear algebra, given rinv = 1 / d (see LA_EXACT_QUOTIENTS)
+__device__ __forceinline__ double la_quot(double x, double d, double rinv) {
+  return LA_EXACT_QUOTIENTS ? x / d : x * rinv;
+}
+// 0.5 / sqrt(t) of qrsolv's Givens rotations (t in [0.25, 0.5]): 0.5 * rsqrt(t) in the
+// contracted build
+__device__ __forceinline__ double la_half_rsqrt(double t) {
+  return LA_EXACT_QUOTIENTS ? 0.5 / sqrt(t) : 0.5 * rsqrt(t);
+}
 
 constexpr double LM_FTOL = 1.49012e-08;
 constexpr double LM_XTOL = 1.49012e-08;
@@ -196,9 +211,10 @@ __device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], doubl
     double ajnorm = sqrt(wsum(p));
     if (ajnorm != 0.0) {
       if (bcast(a[0][j], j) < 0.0) ajnorm = -ajnorm;
+      const double rinv = 1.0 / ajnorm;
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
-        if (row_ge(lane, k, j)) a[k][j] = a[k][j] / ajnorm;
+        if (row_ge(lane, k, j)) a[k][j] = la_quot(a[k][j], ajnorm, rinv);
       if (lane == j) a[0][j] = a[0][j] + 1.0;
       if constexpr (true) {
         double d[N];
@@ -214,9 +230,10 @@ __device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], doubl
         }
         wsum_from(d, j + 1);
         const double ajj = bcast(a[0][j], j);
+        const double rajj = 1.0 / ajj;
 #pragma unroll
         for (int c = j + 1; c < N; ++c) {
-          const double temp = d[c] / ajj;
+          const double temp = la_quot(d[c], ajj, rajj);
 #pragma unroll
           for (int k = 0; k < MPL; ++k)
             if (row_ge(lane, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
@@ -268,11 +285,11 @@ __device__ __forceinline__ void qrsolv(double (&r)[N][N], const int (&ipvt)[N],
           double sn, cs;
           if (fabs(r[k][k]) < fabs(sdiag[k])) {
             const double cotan = r[k][k] / sdiag[k];
-            sn = 0.5 / sqrt(0.25 + 0.25 * (cotan * cotan));
+            sn = la_half_rsqrt(0.25 + 0.25 * (cotan * cotan));
             cs = sn * cotan;
           } else {
             const double tn = sdiag[k] / r[k][k];
-            cs = 0.5 / sqrt(0.25 + 0.25 * (tn * tn));
+            cs = la_half_rsqrt(0.25 + 0.25 * (tn * tn));
             sn = cs * tn;
           }
           r[k][k] = cs * r[k][k] + sn * sdiag[k];
@@ -348,10 +365,11 @@ __device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
   }
   double parl = 0.0;
   if (nsing >= N) {
+    const double rdx = 1.0 / dxnorm;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int l = ipvt[j];
-      wa1[j] = sel(diag, l) * (sel(wa2, l) / dxnorm);
+      wa1[j] = sel(diag, l) * la_quot(sel(wa2, l), dxnorm, rdx);
     }
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -390,10 +408,11 @@ __device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
     const double temp = fp;
     fp = dxnorm - delta;
     if (fabs(fp) <= 0.1 * delta || (parl == 0.0 && fp <= temp && temp < 0.0) || iter == 10) break;
+    const double rdx = 1.0 / dxnorm;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int l = ipvt[j];
-      wa1[j] = sel(diag, l) * (sel(wa2, l) / dxnorm);
+      wa1[j] = sel(diag, l) * la_quot(sel(wa2, l), dxnorm, rdx);
     }
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -446,8 +465,9 @@ __device__ __forceinline__ LMResult lmdif(const Fn& fcn, double (&x)[N], int max
       x[j] = temp + h;
       fcn(x, wa4);
       x[j] = temp;
+      const double rh = 1.0 / h;
 #pragma unroll
-      for (int k = 0; k < MPL; ++k) fjac[k][j] = (wa4[k] - fvec[k]) / h;
+      for (int k = 0; k < MPL; ++k) fjac[k][j] = la_quot(wa4[k] - fvec[k], h, rh);
     }
     nfev += N;
     LM_T0(t_qr);

@@ -23,10 +23,10 @@ Bar (SURVEY.md §8(a) parity classes):
     ITSELF there -- the same candidate scored twice in one process moves s10/s11 in 4-18% of
     rows (tests/test_oracle_golden.py, DESIGN.md §4);
   * fresh (non-golden) batches are checked against the oracle the same way with that
-    batch's own perturbation data, one stable candidate per score excepted: a candidate
-    stable under the seven deterministic perturbations can still change basin under
-    per-step ulp noise -- tools/basin_probe.py shows the reference itself reaching the GPU's
-    value for the one lp=200 candidate this allowance covers (profiles/).
+    batch's own perturbation data; the one exception is s9 of the lp = 200 batch, where
+    tools/basin_probe.py showed a candidate that is stable under the seven deterministic
+    perturbations reaching the GPU's value in the reference itself under per-step ulp noise
+    (profiles/r02_basin_probe_lp200.txt): one row allowed there.
 """
 import json
 import os
@@ -61,9 +61,10 @@ def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(),
     where numpy's BLAS dot products sum in another order than a power-of-two tree (the
     difference is an ulp).  rmax: (n, 22) per-candidate reference movement under the
     perturbations: row-conditioned parity on the stable candidates, of which stable_slack
-    per score may still differ (fresh batches: a candidate that is stable under the seven
-    deterministic perturbations can still change basin under per-step noise, see
-    tools/basin_probe.py)."""
+    ({score number: rows}) may still differ: only where tools/basin_probe.py showed a
+    candidate that is stable under the seven deterministic perturbations changing basin
+    under per-step noise in the reference itself (s9 at lp = 200,
+    profiles/r02_basin_probe_lp200.txt)."""
     gok = (st & 0xFF) == 0
     assert np.array_equal(gok, ref_ok), f"{tag}: failure pattern differs"
     got, ref = out[gok], ref[gok]
@@ -82,7 +83,12 @@ def check_against(out, st, ref, ref_ok, tag, floor, bitexact=BITEXACT, close=(),
             continue
         if stable is not None and j not in SELF_NOISY:
             bad = np.where(stable[:, j] & (r[:, j] > 1e-5))[0]
-            assert len(bad) <= stable_slack, (f"{tag}: s{j + 1} beyond 1e-5 on {len(bad)} candidates where "
+            if len(bad) and os.environ.get("PFE_PARITY_LOG"):
+                with open(os.environ["PFE_PARITY_LOG"], "a") as f:
+                    f.write(json.dumps({"tag": tag, "score": j + 1, "rows": bad.tolist(),
+                                        "rel": r[bad, j].tolist()}) + "\n")
+            allow = stable_slack.get(j + 1, 0) if isinstance(stable_slack, dict) else stable_slack
+            assert len(bad) <= allow, (f"{tag}: s{j + 1} beyond 1e-5 on {len(bad)} candidates where "
                                    f"the reference is stable (rows {bad[:10].tolist()})")
         for tol, key in ((1e-5, "moved_1e-5"), (1e-3, "moved_1e-3")):
             moved = (r[:, j] > tol).mean()
@@ -108,7 +114,7 @@ def test_vs_oracle_fresh_inputs(engine):
     ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
-    check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", floor, rmax=rmax, stable_slack=1)
+    check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", floor, rmax=rmax)
 
 
 @pytest.mark.parametrize("lp,n", [(256, 96), (100, 64), (200, 48), (512, 24)])
@@ -124,19 +130,43 @@ def test_vs_oracle_other_lengths(engine, lp, n):
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
     check_against(out, st, ref, (rst & 0xFF) == 0, f"oracle lp={lp}", floor,
-                  bitexact=exact, close=() if pow2 else (19, 21), rmax=rmax, stable_slack=1)
+                  bitexact=exact, close=() if pow2 else (19, 21), rmax=rmax,
+                  stable_slack={9: 1} if lp == 200 else 0)
 
 
-def test_batched_solver_bit_identical(engine):
-    """The batched lmdif kernels (lm_batch.h) reproduce the wave-per-fit kernels bit for bit
-    (handle option solver = wave / batched)."""
+def lm_columns_agree(o0, s0, o1, s1, floor, slack=0.03, tag=""):
+    """Two GPU solvers on the same candidates: same failures, the bit-exact columns
+    identical, the LM columns different by > 1e-5 on no more rows than 1.5 x the reference's
+    own 1-ulp floor for that profile length + `slack` (both solvers sum their m-rows in
+    another order than MINPACK and contract the solver's linear algebra into FMAs, so on
+    the chaotic rows each lands on one of the reference's own nearby values)."""
+    assert np.array_equal(s0, s1), tag
+    ok = (s0 & 0xFF) == 0
+    r = rel_err(o1[ok], o0[ok])
+    for j in BITEXACT:
+        assert (r[:, j] == 0).all(), f"{tag} s{j + 1}"
+    for j in range(22):
+        if j not in BITEXACT:
+            moved = (r[:, j] > 1e-5).mean()
+            assert moved <= 1.5 * floor["moved_1e-5"][j] + slack, f"{tag} s{j + 1}: {moved:.3f}"
+
+
+def floor_for(lp):
+    """The reference's 1-ulp chaos floor of the golden set nearest in profile length."""
+    return FLOOR["bates22_superb64"] if lp <= 64 else FLOOR["bates22_phcx128"]
+
+
+def test_batched_solver_matches_wave_solver(engine):
+    """The batched lmdif kernels (lm_batch.h) against the wave-per-fit kernels (handle option
+    solver = wave / batched).  Without FMA contraction of the solver's linear algebra
+    (libpfe_nofma builds) the two are bit-identical; with it, the compiler contracts each
+    inlined code shape on its own, so they are held to lm_columns_agree."""
     b = bates_batch(200, seed=21)
     with engine.options(solver="wave"):
         o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     with engine.options(solver="batched"):
         o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    assert np.array_equal(s0, s1)
-    assert np.array_equal(np.nan_to_num(o0, nan=7.0), np.nan_to_num(o1, nan=7.0))
+    lm_columns_agree(o0, s0, o1, s1, floor_for(128), tag="wave vs batched")
 
 
 def test_concurrent_groups_and_hand_over_bit_identical(engine):
@@ -189,15 +219,7 @@ def test_pooled_group_solver(engine, lp, n):
     with engine.options(solver="batched"):
         o0, s0 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     o1, s1 = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    assert np.array_equal(s0, s1)
-    ok = (s0 & 0xFF) == 0
-    r = rel_err(o1[ok], o0[ok])
-    for j in BITEXACT:
-        assert (r[:, j] == 0).all(), f"s{j + 1}"
-    floor = FLOOR["bates22_phcx128"]
-    for j in range(22):
-        if j not in BITEXACT:
-            assert (r[:, j] > 1e-5).mean() <= 1.5 * floor["moved_1e-5"][j] + 0.03, f"s{j + 1}"
+    lm_columns_agree(o0, s0, o1, s1, floor_for(lp), tag=f"pooled vs batched lp={lp}")
     # pool independence: the same candidates in another order and batch size
     perm = np.random.default_rng(1).permutation(len(b["prof"]))[:n * 5 // 12]
     o2, s2 = engine.bates22(b["prof"][perm], b["sub"][perm], b["dmcurve"][perm], b["scal"][perm])
@@ -241,8 +263,7 @@ def test_wide_histograms_vs_oracle(engine):
     ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
-    check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor, rmax=rmax,
-                  stable_slack=1)
+    check_against(out, st, ref, (rst & 0xFF) == 0, "wide histograms", floor, rmax=rmax)
 
 
 def test_pooled_tiny_and_empty_batches(engine):
@@ -290,5 +311,4 @@ def test_config3_full_size_10m(engine):
                                             b["scal"][:k], workers=8)
     gold = FLOOR["bates22_phcx128"]
     floor = {kk: np.maximum(own[kk], gold[kk]).tolist() for kk in gold if kk.startswith("moved")}
-    check_against(o0, s0, ref, (rst & 0xFF) == 0, "config 3 @10M, tile 0", floor, rmax=rmax,
-                  stable_slack=1)
+    check_against(o0, s0, ref, (rst & 0xFF) == 0, "config 3 @10M, tile 0", floor, rmax=rmax)

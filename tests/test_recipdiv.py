@@ -1,4 +1,4 @@
-"""Host check of the shared-divisor quotient the Gaussian models use (bates_gauss.hip RecipDiv):
+"""Host check of the shared-divisor quotient the Gaussian models use (bates_gauss.h RecipDiv):
 with y = RN(1/b), q = RN(a*y), r = fma(-q, b, a), t = fma(r, y, q) equals the IEEE quotient
 a/b bit for bit inside the kernel's guard (|b| in [2^-500, 2^500], |a| in [2^-900, 2^401])
 -- Markstein's theorem, checked here on random and adversarial operands with the host's fma."""

@@ -8,6 +8,13 @@ cost per residual element and the residual count m per solve group are stated be
 add/sub/mul/div/sqrt/exp/sin counts as one operation.
 
   python tools/bates_flops.py gpurun_out/lmprof.json > profiles/r01_bates22_flops.json
+  python tools/bates_flops.py --pfd gpurun_out/r03_lmprof_pfd22.json > profiles/r03_pfd22_ops.json
+
+--pfd: the PFD 22-score path (PFDFile.compute, PFDFile.py:587-613) on bench.py's 16 x 32 x 128
+folds: the same Gaussian / sine fits on the float 0..255 profile (histogram widths measured on
+that profile), the PFD DM-curve fit (PFDOperations.getDMFittings :274-393: N = 4, m = 100
+trial DMs, 14 operations per residual), and the fold arithmetic of pfe_pfd_dmprof (part sums,
+the 100-DM chi^2 sweep) plus the sub-band correlations as non-LM work.
 """
 import json
 import sys
@@ -62,13 +69,50 @@ def mean_hist_bins(n=2000, lp=128):
     return float(np.mean(hp)), float(np.mean(hd))
 
 
+PFD_SHAPE = (16, 32, 128)  # npart x nsub x proflen of bench.py --path pfd22
+PFD_NDM = 100              # PFDFile.plot_chi2_vs_DM trial DMs
+
+
+def pfd_groups():
+    g = {k: v for k, v in GROUPS.items() if not k.startswith("sine_dm_sub/N=3")}
+    g["pfd22/N=4"] = (14, PFD_NDM, "PFD DM-curve fit (getDMFittings, m = 100 trial DMs)")
+    return g
+
+
+def mean_hist_bins_pfd(n=300):
+    """FD widths of the PFD profile (pfe_pfd_dmprof's 0..255 float profile) and its
+    derivative, over bench.py's synthetic folds."""
+    root = __file__.rsplit("/tools/", 1)[0]
+    sys.path.insert(0, root)
+    from bench import pfd_block
+    from oracle.bates import backward_diff, fd_bins
+    from oracle.pfd import PFDState
+
+    hp, hd = [], []
+    for d in pfd_block(n, PFD_SHAPE, 20261019):
+        p = np.asarray(PFDState(d).profile(), dtype=np.float64)
+        hp.append(fd_bins(p))
+        hd.append(fd_bins(backward_diff(p)))
+    return float(np.mean(hp)), float(np.mean(hd))
+
+
+def pfd_other_ops():
+    npart, nsub, L = PFD_SHAPE
+    parts = npart * nsub * L            # part sums (dedisperse at the best DM)
+    sweep = PFD_NDM * (nsub * L + 3 * L)  # per trial DM: rotated sub-band sums + chi^2
+    sub = 120 * L * 6 + 17 * L * 6 + 20 * L  # sub-band correlations, boxcars
+    return parts + sweep + sub + 16 * L * 3
+
+
 def main():
-    prof = json.load(open(sys.argv[1]))
-    hp, hd = mean_hist_bins()
+    pfd = "--pfd" in sys.argv
+    src = [a for a in sys.argv[1:] if not a.startswith("--")][0]
+    prof = json.load(open(src))
+    hp, hd = mean_hist_bins_pfd() if pfd else mean_hist_bins()
     n_cand = prof["gauss/N=8"]["calls"]
     total = 0.0
     groups = {}
-    for key, (c_model, m, what) in GROUPS.items():
+    for key, (c_model, m, what) in (pfd_groups() if pfd else GROUPS).items():
         g = prof[key]
         if m is None:
             m = hp if key == "gauss/N=2" else 0.5 * (hp + hd)
@@ -85,11 +129,11 @@ def main():
                        "ops_per_solve": per_solve, "ops_per_candidate": per_solve * calls}
         total += per_solve * calls
     # non-LM work: histograms, percentiles, boxcars, 120 sub-band correlations, chi^2 sums
-    other = 16 * 128 * 3 + 120 * 128 * 6 + 17 * 128 * 6 + 20 * 128
+    other = pfd_other_ops() if pfd else 16 * 128 * 3 + 120 * 128 * 6 + 17 * 128 * 6 + 20 * 128
     print(json.dumps({"ops_per_candidate": total + other, "lm_ops_per_candidate": total,
                       "other_ops_per_candidate": other, "mean_hist_bins_profile": hp,
                       "mean_hist_bins_dy": hd, "groups": groups,
-                      "source": sys.argv[1]}, indent=1))
+                      "source": src, "path": "pfd22" if pfd else "bates22"}, indent=1))
 
 
 if __name__ == "__main__":
