@@ -1,7 +1,7 @@
 """ScoreGenerator-compatible command line (ScoreGenerator.py:99-292), batched on the GPU.
 
   python -m pulsarfeatureextractor_amd.cli -c <dir|file> -o <out> [--phcx|--superb]
-         [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K]
+         [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K] [--start K]
 
 Same flags, same output-file probing (:147-160), same mode dispatch (:215-290), for PHCX,
 SUPERB and PFD files in every mode, --label included (its prompt is commented out in the
@@ -30,6 +30,9 @@ def main(argv=None):
     p.add_option("--dmprof", action="store_true", dest="dmprof", default=False)
     p.add_option("--device", action="store", dest="device", type="int", default=0)
     p.add_option("--workers", action="store", dest="workers", type="int", default=None)
+    # resume offset (not in the reference): skip the first K discovered candidates, e.g. the
+    # ones a stopped collective run had already appended to its output file
+    p.add_option("--start", action="store", dest="start", type="int", default=0)
     args, _ = p.parse_args(argv)
     # output-file probing (:147-160)
     single_file = os.path.exists(args.outputPath)
@@ -50,7 +53,7 @@ def main(argv=None):
     from .candidate import get_engine
 
     get_engine(args.device)
-    dp = processor.DataProcessor(args.verbose, workers=args.workers)
+    dp = processor.DataProcessor(args.verbose, workers=args.workers, start=args.start)
     phcx, pfd, superb = args.phcx, args.pfd, args.superb
     try:
         if args.label:  # :220-225 (labelPFD with the two arguments ScoreGenerator passes)

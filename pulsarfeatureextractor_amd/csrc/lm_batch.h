@@ -203,6 +203,7 @@ __device__ __forceinline__ void blm_init(const Fn& fcn, int f, BlmState<N, FPW>&
 // SIMT phase for this lane's fit: lmpar, the trial point and the predicted-reduction terms
 template <int N, int FPW>
 __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
+  PFE_LA_CONTRACT
   double r[N][N], diag[N], qtf[N], x[N];
   int ipvt[N];
 #pragma unroll
@@ -224,13 +225,14 @@ __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
     for (int j = 0; j < N; ++j) acn[j] = S.acn[j][f];
     double gnorm = 0.0;
     if (fnorm != 0.0) {
+      const double rfn = 1.0 / fnorm;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         const double wl = sel(acn, ipvt[j]);
         if (wl != 0.0) {
           double sum = 0.0;
 #pragma unroll
-          for (int i = 0; i <= j; ++i) sum += r[i][j] * (qtf[i] / fnorm);
+          for (int i = 0; i <= j; ++i) sum += r[i][j] * la_quot(qtf[i], fnorm, rfn);
           gnorm = fmax(gnorm, fabs(sum / wl));
         }
       }

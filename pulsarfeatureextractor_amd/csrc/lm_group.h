@@ -231,8 +231,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         if (rdiag[c] != 0.0) {
           const double t2 = gbcast<G>(a[0][c], j) / rdiag[c];
           rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
-          const double q = rdiag[c] / wa[c];
-          if (0.05 * (q * q) <= EPSMCH) {
+          if (la_norm_lost(rdiag[c], wa[c])) {
             double r = 0.0;
 #pragma unroll
             for (int k = 0; k < MPL; ++k)

@@ -27,8 +27,10 @@
 // The residual models and every bit-exact score keep -ffp-contract=off (numpy evaluates each
 // operation rounded).  -DPFE_LA_NOFMA restores the uncontracted solver (A/B builds).
 // For the same reason the quotients by one per-column divisor (the forward-difference step h
-// of fdjac2, the Householder norm of qrfac) are products with its reciprocal: one division
-// per column instead of one per row.
+// of fdjac2, the Householder norm of qrfac and its column updates, lmpar's dxnorm, the gtol
+// test's fnorm) are products with its reciprocal, qrsolv's Givens rotations take 0.5 *
+// rsqrt, qrfac's norm-loss test compares squares, and enorm of an n-vector whose elements all
+// lie in MINPACK's intermediate range is sqrt(sum x^2) without per-element branches.
 #ifdef PFE_LA_NOFMA
 #define PFE_LA_CONTRACT
 constexpr bool LA_EXACT_QUOTIENTS = true;
@@ -39,22 +41,31 @@ constexpr bool LA_EXACT_QUOTIENTS = false;
 
 namespace pfe {
 
-// x / d of the solver's linear algebra, given rinv = 1 / d (see LA_EXACT_QUOTIENTS)
-__device__ __forceinline__ double la_quot(double x, double d, double rinv) {
-  return LA_EXACT_QUOTIENTS ? x / d : x * rinv;
-}
-// 0.5 / sqrt(t) of qrsolv's Givens rotations (t in [0.25, 0.5]): 0.5 * rsqrt(t) in the
-// contracted build
-__device__ __forceinline__ double la_half_rsqrt(double t) {
-  return LA_EXACT_QUOTIENTS ? 0.5 / sqrt(t) : 0.5 * rsqrt(t);
-}
-
 constexpr double LM_FTOL = 1.49012e-08;
 constexpr double LM_XTOL = 1.49012e-08;
 constexpr double LM_GTOL = 0.0;
 constexpr double LM_FACTOR = 100.0;
 constexpr double EPSMCH = 2.220446049250313e-16;
 constexpr double DWARF = 2.2250738585072014e-308;
+
+// x / d of the solver's linear algebra, given rinv = 1 / d (see LA_EXACT_QUOTIENTS)
+__device__ __forceinline__ double la_quot(double x, double d, double rinv) {
+  return LA_EXACT_QUOTIENTS ? x / d : x * rinv;
+}
+// qrfac's test that a downdated column norm lost too much to be trusted,
+// 0.05 (rdiag / wa)^2 <= epsmch: without the quotient in the contracted build (wa > 0)
+__device__ __forceinline__ bool la_norm_lost(double rdiag, double wa) {
+  if (LA_EXACT_QUOTIENTS) {
+    const double q = rdiag / wa;
+    return 0.05 * (q * q) <= EPSMCH;
+  }
+  return 0.05 * (rdiag * rdiag) <= EPSMCH * (wa * wa);
+}
+// 0.5 / sqrt(t) of qrsolv's Givens rotations (t in [0.25, 0.5]): 0.5 * rsqrt(t) in the
+// contracted build
+__device__ __forceinline__ double la_half_rsqrt(double t) {
+  return LA_EXACT_QUOTIENTS ? 0.5 / sqrt(t) : 0.5 * rsqrt(t);
+}
 
 // ---- optional phase-cycle profiler (instrumented builds only: -DPFE_LM_PROFILE) ----------
 // Per translation unit, per parameter count N (slot 0..3 for N = 2, 3, 4, 8): counters
@@ -102,8 +113,21 @@ template <int N>
 __device__ __forceinline__ double enorm_u(const double (&x)[N]) {
   PFE_LA_CONTRACT
   const double rdwarf = 3.834e-20, rgiant = 1.304e19;
-  double s1 = 0, s2 = 0, s3 = 0, x1max = 0, x3max = 0;
   const double agiant = rgiant / (double)N;
+  if constexpr (!LA_EXACT_QUOTIENTS) {
+    // every non-zero element in MINPACK's intermediate range (the common case): enorm is
+    // sqrt(sum x^2) there, with no per-element branches
+    double s = 0.0;
+    bool mid = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const double xabs = fabs(x[i]);
+      s += xabs * xabs;
+      mid = mid && ((xabs > rdwarf && xabs < agiant) || xabs == 0.0);
+    }
+    if (mid) return sqrt(s);
+  }
+  double s1 = 0, s2 = 0, s3 = 0, x1max = 0, x3max = 0;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const double xabs = fabs(x[i]);
@@ -240,8 +264,7 @@ __device__ __forceinline__ void qrfac(double (&a)[MPL][N], int (&ipvt)[N], doubl
           if (rdiag[c] != 0.0) {
             const double t2 = bcast(a[0][c], j) / rdiag[c];
             rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
-            const double q = rdiag[c] / wa[c];
-            if (0.05 * (q * q) <= EPSMCH) {
+            if (la_norm_lost(rdiag[c], wa[c])) {
               double r = 0.0;
 #pragma unroll
               for (int k = 0; k < MPL; ++k)
