@@ -52,8 +52,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (counts an FMA as 2 operations)
-# -ffp-contract=off (parity with numpy's individually rounded operations): no FMA is issued,
-# so one operation per lane per cycle is the attainable VALU ceiling
+# the residual models run with -ffp-contract=off (parity with numpy's individually rounded
+# operations; only the solver's linear algebra is contracted), so one operation per lane per
+# cycle is the ceiling that applies to most of the work
 FP64_NOFMA_TOPS = 39.3
 
 
@@ -100,8 +101,9 @@ def load_traffic(name: str):
         return None
 
 
-def load_ops_per_candidate():
-    p = os.path.join(ROOT, "profiles", "r01_bates22_ops.json")
+def load_ops_per_candidate(name="r01_bates22_ops.json"):
+    """Frozen algorithmic fp64 operation count per candidate (tools/bates_flops.py)."""
+    p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             return json.load(f)["ops_per_candidate"]
@@ -439,8 +441,9 @@ def run_lyon8(ctx, args, n, lp):
     }, out
 
 
-def bates_roofline(n, kern_ms, kern_max, kernel):
-    ops = load_ops_per_candidate()
+def bates_roofline(n, kern_ms, kern_max, kernel, ops=None):
+    if ops is None:
+        ops = load_ops_per_candidate()
     achieved = (ops * n / (kern_ms * 1e-3) / 1e12) if ops else None
     return {
         "bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -452,7 +455,7 @@ def bates_roofline(n, kern_ms, kern_max, kernel):
         "note": "algorithmic fp64 operations (add/mul/div/sqrt/exp/sin = 1 each, "
                 "tools/bates_flops.py) per second; frac against the 78.6 TFLOP/s FMA peak and "
                 "frac_nofma_valu against the 39.3 Tops/s one-op-per-lane ceiling that applies "
-                "with -ffp-contract=off",
+                "to the uncontracted residual models (the solver's linear algebra is contracted)",
         "avg_step_ms": kern_ms, "avg_step_ms_max_over_ranks": kern_max,
     }
 
@@ -855,6 +858,15 @@ def main():
                 ctx.eng.pfd_bates22(tp, tf, ts, out=out, status=status)
 
             elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+            ops = (load_ops_per_candidate("r03_pfd22_ops.json")
+                   if pfd_shape == (16, 32, 128) else None)
+            roof = bates_roofline(n, kern_ms, kern_max, "pfe_pfd_bates22 (9 kernels, one step)",
+                                  ops=ops)
+            roof["note"] = ("algorithmic fp64 operations of PFDFile.compute on 16x32x128 folds "
+                            "(tools/bates_flops.py --pfd -> profiles/r03_pfd22_ops.json: the "
+                            "fits' solve statistics from the instrumented build, the fold "
+                            "arithmetic of the dedispersion and the 100-DM chi^2 sweep) per "
+                            "second" if ops else "no frozen operation count for this fold shape")
             result = {
                 "metric": "candidates/sec (PFD 22-score path)",
                 **common_fields(ctx, n, args.steps, args.warmup, elapsed),
@@ -862,12 +874,7 @@ def main():
                 "config": {"workload": f"{n} synthetic PRESTO folds per GPU ({npart} parts x "
                                        f"{nsub} sub-bands x {L} bins): PFDFile.compute, 22 scores "
                                        f"(pfe_pfd_bates22)", **common_cfg},
-                "roofline": {"bound": "fp64-valu", "achieved": None, "peak": FP64_PEAK_TFLOPS,
-                             "unit": "TFLOP/s", "frac": None, "traffic": None,
-                             "note": "operation count of the PFD 22-score path not frozen; the "
-                                     "fits are the 22-score path's (see --path bates22)",
-                             "kernel": "pfe_pfd_bates22 (9 kernels, one step)",
-                             "avg_step_ms": kern_ms, "avg_step_ms_max_over_ranks": kern_max},
+                "roofline": roof,
             }
             if want_cpu:
                 result["cpu_baseline"] = cpu_baseline_pfd22(pfd_shape, args.cpu_sample)

@@ -242,8 +242,8 @@ __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
     S.info[f] = info;
     if (info != 0) return;
   }
-  double wa1[N], wa2[N], wa3[N];
-  lmpar<N>(r, ipvt, diag, qtf, delta, par, wa1, wa2);
+  double wa1[N], wa2[N], wa3[N], wp[N];
+  lmpar<N>(r, ipvt, diag, qtf, delta, par, wa1, wa2, wp);
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     wa1[j] = -wa1[j];
@@ -257,7 +257,7 @@ __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
   for (int j = 0; j < N; ++j) wa3[j] = 0.0;
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    temp = sel(wa1, ipvt[j]);
+    temp = -wp[j];  // wa1[ipvt[j]]
 #pragma unroll
     for (int i = 0; i <= j; ++i) wa3[i] = wa3[i] + r[i][j] * temp;
   }

@@ -352,11 +352,12 @@ __device__ __forceinline__ void qrsolv(double (&r)[N][N], const int (&ipvt)[N],
 }
 
 // ---- lmpar (replicated) -----------------------------------------------------------------
+// MINPACK's lmpar step for step (the uncontracted build's; lmpar below)
 template <int N>
-__device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
-                                      const double (&diag)[N], const double (&qtb)[N],
-                                      double delta, double& par, double (&x)[N],
-                                      double (&sdiag)[N]) {
+__device__ __forceinline__ void lmpar_literal(double (&r)[N][N], const int (&ipvt)[N],
+                                              const double (&diag)[N], const double (&qtb)[N],
+                                              double delta, double& par, double (&x)[N],
+                                              double (&sdiag)[N]) {
   PFE_LA_CONTRACT
   double wa1[N], wa2[N];
   int nsing = N;
@@ -450,6 +451,197 @@ __device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
     if (fp < 0.0) paru = fmin(paru, par);
     par = fmax(parl, par + parc);
   }
+}
+
+// qrsolv in the pivoted basis: dp[j] = diag[ipvt[j]], and xp[j] = x[ipvt[j]] on return (the
+// same values as qrsolv's, without its permutation selects)
+template <int N>
+__device__ __forceinline__ void qrsolv_p(double (&r)[N][N], const double (&dp)[N],
+                                         const double (&qtb)[N], double (&xp)[N],
+                                         double (&sdiag)[N]) {
+  PFE_LA_CONTRACT
+  double wa[N], rd[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+#pragma unroll
+    for (int i = j; i < N; ++i) r[i][j] = r[j][i];
+    rd[j] = r[j][j];
+    wa[j] = qtb[j];
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double dl = dp[j];
+    if (dl != 0.0) {
+#pragma unroll
+      for (int k = j; k < N; ++k) sdiag[k] = 0.0;
+      sdiag[j] = dl;
+      double qtbpj = 0.0;
+#pragma unroll
+      for (int k = j; k < N; ++k) {
+        if (sdiag[k] != 0.0) {
+          double sn, cs;
+          if (fabs(r[k][k]) < fabs(sdiag[k])) {
+            const double cotan = r[k][k] / sdiag[k];
+            sn = la_half_rsqrt(0.25 + 0.25 * (cotan * cotan));
+            cs = sn * cotan;
+          } else {
+            const double tn = sdiag[k] / r[k][k];
+            cs = la_half_rsqrt(0.25 + 0.25 * (tn * tn));
+            sn = cs * tn;
+          }
+          r[k][k] = cs * r[k][k] + sn * sdiag[k];
+          const double temp = cs * wa[k] + sn * qtbpj;
+          qtbpj = -sn * wa[k] + cs * qtbpj;
+          wa[k] = temp;
+#pragma unroll
+          for (int i = k + 1; i < N; ++i) {
+            const double t = cs * r[i][k] + sn * sdiag[i];
+            sdiag[i] = -sn * r[i][k] + cs * sdiag[i];
+            r[i][k] = t;
+          }
+        }
+      }
+    }
+    sdiag[j] = r[j][j];
+    r[j][j] = rd[j];
+  }
+  int nsing = N;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (sdiag[j] == 0.0 && nsing == N) nsing = j;
+    if (nsing < N) wa[j] = 0.0;
+  }
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    if (j < nsing) {
+      double sum = 0.0;
+#pragma unroll
+      for (int i = j + 1; i < N; ++i)
+        if (i < nsing) sum += r[i][j] * wa[i];
+      wa[j] = (wa[j] - sum) / sdiag[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) xp[j] = wa[j];
+}
+
+// lmpar.  x: the Levenberg-Marquardt step (natural order), xp[j] = x[ipvt[j]].  The contracted
+// build works in the pivoted basis throughout -- diag[ipvt[j]] selected once, qrsolv_p, the
+// scaled step and its norm in pivoted order (a norm does not depend on the order but for its
+// rounding) -- and scatters x once at the end, instead of MINPACK's per-iteration
+// permutations (on a replicated register array each is an n-way select chain: for n = 8
+// about 500 instructions per iteration)
+template <int N>
+__device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
+                                      const double (&diag)[N], const double (&qtb)[N],
+                                      double delta, double& par, double (&x)[N],
+                                      double (&sdiag)[N], double (&xp)[N]) {
+  PFE_LA_CONTRACT
+  if constexpr (LA_EXACT_QUOTIENTS) {
+    lmpar_literal<N>(r, ipvt, diag, qtb, delta, par, x, sdiag);
+#pragma unroll
+    for (int j = 0; j < N; ++j) xp[j] = sel(x, ipvt[j]);
+    return;
+  }
+  double dp[N], wa1[N], wa2[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) dp[j] = sel(diag, ipvt[j]);
+  int nsing = N;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    wa1[j] = qtb[j];
+    if (r[j][j] == 0.0 && nsing == N) nsing = j;
+    if (nsing < N) wa1[j] = 0.0;
+  }
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    if (j < nsing) {
+      wa1[j] = wa1[j] / r[j][j];
+      const double temp = wa1[j];
+#pragma unroll
+      for (int i = 0; i < j; ++i) wa1[i] = wa1[i] - r[i][j] * temp;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    xp[j] = wa1[j];
+    wa2[j] = dp[j] * xp[j];
+  }
+  int iter = 0;
+  double dxnorm = enorm_u(wa2);
+  double fp = dxnorm - delta;
+  if (fp <= 0.1 * delta) {
+    par = 0.0;  // iter == 0
+  } else {
+    double parl = 0.0;
+    if (nsing >= N) {
+      const double rdx = 1.0 / dxnorm;
+#pragma unroll
+      for (int j = 0; j < N; ++j) wa1[j] = dp[j] * (wa2[j] * rdx);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        double sum = 0.0;
+#pragma unroll
+        for (int i = 0; i < j; ++i) sum += r[i][j] * wa1[i];
+        wa1[j] = (wa1[j] - sum) / r[j][j];
+      }
+      const double temp = enorm_u(wa1);
+      parl = ((fp / delta) / temp) / temp;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      double sum = 0.0;
+#pragma unroll
+      for (int i = 0; i <= j; ++i) sum += r[i][j] * qtb[i];
+      wa1[j] = sum / dp[j];
+    }
+    const double gnorm = enorm_u(wa1);
+    double paru = gnorm / delta;
+    if (paru == 0.0) paru = DWARF / fmin(delta, 0.1);
+    par = fmax(par, parl);
+    par = fmin(par, paru);
+    if (par == 0.0) par = gnorm / dxnorm;
+    for (;;) {
+      ++iter;
+      if (par == 0.0) par = fmax(DWARF, 0.001 * paru);
+      const double sp = sqrt(par);
+#pragma unroll
+      for (int j = 0; j < N; ++j) wa1[j] = sp * dp[j];
+      qrsolv_p<N>(r, wa1, qtb, xp, sdiag);
+      LM_ADD(3, 1);
+#pragma unroll
+      for (int j = 0; j < N; ++j) wa2[j] = dp[j] * xp[j];
+      dxnorm = enorm_u(wa2);
+      const double temp = fp;
+      fp = dxnorm - delta;
+      if (fabs(fp) <= 0.1 * delta || (parl == 0.0 && fp <= temp && temp < 0.0) || iter == 10) break;
+      const double rdx = 1.0 / dxnorm;
+#pragma unroll
+      for (int j = 0; j < N; ++j) wa1[j] = dp[j] * (wa2[j] * rdx);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        wa1[j] = wa1[j] / sdiag[j];
+        const double t = wa1[j];
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) wa1[i] = wa1[i] - r[i][j] * t;
+      }
+      const double t = enorm_u(wa1);
+      const double parc = ((fp / delta) / t) / t;
+      if (fp > 0.0) parl = fmax(parl, par);
+      if (fp < 0.0) paru = fmin(paru, par);
+      par = fmax(parl, par + parc);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) put(x, ipvt[j], xp[j]);
+}
+template <int N>
+__device__ __forceinline__ void lmpar(double (&r)[N][N], const int (&ipvt)[N],
+                                      const double (&diag)[N], const double (&qtb)[N],
+                                      double delta, double& par, double (&x)[N],
+                                      double (&sdiag)[N]) {
+  double xp[N];
+  lmpar<N>(r, ipvt, diag, qtb, delta, par, x, sdiag, xp);
 }
 
 // ---- lmdif ----------------------------------------------------------------------------

@@ -75,9 +75,11 @@ def test_pfd_candidate(tmp_path):
             prof = c.calculateProfileStatScores(False)
             dm = c.calculateDMCurveStatScores(False)
             ref = g["lyon8"][i]
-            assert prof[0] == ref[0] and prof[1] == ref[1]
-            assert abs(dm[0] - ref[4]) <= 1e-6 * abs(ref[4])
+            # bit-exact, NaN where the reference's is (a flat fold: 0/0 in the 0..255 scaling)
+            assert np.array_equal(np.array(prof[:2]), ref[:2], equal_nan=True), (i, prof, ref[:4])
+            assert (abs(dm[0] - ref[4]) <= 1e-6 * abs(ref[4])
+                    or (np.isnan(dm[0]) and np.isnan(ref[4]))), (i, dm[0], ref[4])
         if g["bates22_ok"][i]:
             s = c.calculateScores(False)
             for j in (2, 3, 11, 12, 13, 14, 15, 18, 19):
-                assert s[j] == g["bates22"][i][j], (i, j)
+                assert s[j] == g["bates22"][i][j] or (np.isnan(s[j]) and np.isnan(g["bates22"][i][j])), (i, j)
