@@ -37,7 +37,9 @@ Besides the contract fields the JSON line carries:
                                   the measured H2D bandwidth of the box
                    lyon8_phcx -- the 8 Lyon features at the real PHCX shape: 128-bin profile
                                  + the whole 128 x 128 DataBlock as the DM array (16 KiB rows,
-                                 lyon8_u8_long), with its HBM roofline
+                                 lyon8_u8_pow2), with its HBM roofline
+                   lyon8_phcx_ndm120 -- the same with a 120 x 128 DataBlock (15 360-byte
+                                        rows, lyon8_u8_lds)
 """
 from __future__ import annotations
 
@@ -627,7 +629,9 @@ def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2)
                     f"(a whole 128 x 128 PHCX DataBlock), 8 Lyon features (pfe_lyon8_u8)",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": f"pfe::lyon8_u8_long<{lp}, 128, {ld // (64 * 128)}>",
+                     "kernel": (f"pfe::lyon8_u8_pow2<{lp}, {ld // 1024}>" if ld in (8192, 16384)
+                                else f"pfe::lyon8_u8_lds<{lp}, 112>" if ld == 15360
+                                else f"pfe::lyon8_u8_lds or lyon8_u8_long<{lp}>"),
                      "algorithmic_bytes_per_candidate": per_cand,
                      "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max},
     }
@@ -759,6 +763,9 @@ def main():
             extra["config2_e2e"] = run_e2e(ctx, args, n, lp)
             torch.cuda.empty_cache()
             extra["lyon8_phcx"] = run_lyon8_phcx(ctx, args)
+            torch.cuda.empty_cache()
+            # nDM = 120 (the golden dmplane's shape): 15 360-byte DataBlock
+            extra["lyon8_phcx_ndm120"] = run_lyon8_phcx(ctx, args, ld=15360)
     elif args.path == "bates22":
         result, out = run_bates22(ctx, args, n, lp, args.steps, args.warmup)
         if want_cpu:

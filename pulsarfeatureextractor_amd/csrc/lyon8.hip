@@ -413,6 +413,309 @@ __global__ __launch_bounds__(256) void lyon8_u8_long(const uint8_t* __restrict__
   }
 }
 
+// ---- long DM rows of 2^k bytes: coalesced, no per-byte floating point -------------------
+// nDM = 64 / 128 DataBlock rows (ld = 8192 / 16384 = 1024 * NI).  With n = 2^k the mean
+// S1 / 2^k is exact, and so are d = x - mean (a multiple of 2^-k below 256), d*d and every
+// partial sum inside one 128-value leaf of numpy's pairwise tree (< 2^23 in units of 2^-2k):
+// numpy's leaf sum is the exact rational
+//     2^2k * sum_leaf d^2 = 2^2k B - 2^(k+1) S1 A + 128 S1^2     (A = sum x, B = sum x^2)
+// evaluated here in 64-bit integers and converted exactly (< 2^53).  Only the tree levels
+// above the leaves round, and those follow numpy's order: the two 8192-value chunks (ld =
+// 16384) are each a perfect tree over 64 leaves, added as (0 + c0) + c1 = c0 + c1.
+//   * loads: wave instruction i reads bytes [1024 i, 1024 i + 1024) of the row, 16 B per
+//     lane (fully coalesced dwordx4, all NI issued before any is consumed); lanes 8g..8g+7
+//     hold leaf 8i + g.
+//   * per leaf, A and B over its 8 lanes by a reduce-scatter: for the leaves of instructions
+//     8s..8s+7 lane t = lane & 7 ends with the sums of instruction 8s + t (exact integers),
+//     so each lane converts two leaves (s = 0, 1), not sixteen.
+//   * set s's leaf index within its chunk is 8t + g: numpy's tree pairs leaf bits 0-2 (lane
+//     bits 3-5: row_ror 8, permlane16 / permlane32 swaps) and then leaf bits 3-5 (lane bits
+//     0-2: quad and half-row DPP).  IEEE addition is commutative, so both lanes of every pair
+//     hold the bits numpy's pair sum has.
+//   * skew / kurt / mean as lyon8_u8_long (exact power sums, 128-bit numerators).
+constexpr int DPP_ROW_ROR8 = 0x128;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)dpp_i32<CTRL>((int)v);
+}
+
+// lane t (= lane & 7) of each 8-lane group gets sum over the group of v[t]
+__device__ __forceinline__ uint32_t reduce_scatter8(const uint32_t (&v)[8], int t) {
+  const bool b2 = t & 4, b1 = t & 2, b0 = t & 1;
+  uint32_t a[4], b[2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)  // partner 7 - t: opposite bit 2
+    a[k] = (b2 ? v[k + 4] : v[k]) + dpp_u32<DPP_ROW_HALF_MIRROR>(b2 ? v[k] : v[k + 4]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k)  // partner t ^ 2
+    b[k] = (b1 ? a[k + 2] : a[k]) + dpp_u32<DPP_QUAD_XOR2>(b1 ? a[k] : a[k + 2]);
+  return (b0 ? b[1] : b[0]) + dpp_u32<DPP_QUAD_XOR1>(b0 ? b[0] : b[1]);
+}
+
+__device__ __forceinline__ double swap16_sum(double v) {  // v + (v of lane ^ 16)
+  const long long x = __double_as_longlong(v);
+  const unsigned lo = (unsigned)x, hi = (unsigned)((unsigned long long)x >> 32);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0])) +
+         __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]));
+}
+__device__ __forceinline__ double swap32_sum(double v) {  // v + (v of lane ^ 32)
+  const long long x = __double_as_longlong(v);
+  const unsigned lo = (unsigned)x, hi = (unsigned)((unsigned long long)x >> 32);
+  const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0])) +
+         __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]));
+}
+
+// numpy's pairwise tree over the 64 leaves of a set (leaf 8t + g in lane 8g + t)
+__device__ __forceinline__ double leaf_tree64(double v) {
+  v += dpp_f64<DPP_ROW_ROR8>(v);  // leaf bit 0 = lane bit 3
+  v = swap16_sum(v);              // leaf bit 1 = lane bit 4
+  v = swap32_sum(v);              // leaf bit 2 = lane bit 5
+  v += dpp_f64<DPP_QUAD_XOR1>(v);  // leaf bit 3 = lane bit 0
+  v += dpp_f64<DPP_QUAD_XOR2>(v);  // leaf bit 4 = lane bit 1
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);  // leaf bit 5 = lane bit 2
+  return v;
+}
+
+// y^3 / y^4 power sums of one dword (y = x - 128), as acc2_dword without the udot4 sums
+__device__ __forceinline__ void acc34_dword(uint32_t x, int& t3, uint32_t& t4a) {
+  const uint32_t lo = __builtin_amdgcn_perm(0u, x, 0x0c020c00u);
+  const uint32_t hi = __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
+  short2v ylo = __builtin_bit_cast(short2v, lo) - (short2v){128, 128};
+  short2v yhi = __builtin_bit_cast(short2v, hi) - (short2v){128, 128};
+  ushort2v qlo = __builtin_bit_cast(ushort2v, ylo) * __builtin_bit_cast(ushort2v, ylo);
+  ushort2v qhi = __builtin_bit_cast(ushort2v, yhi) * __builtin_bit_cast(ushort2v, yhi);
+  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qlo), ylo, t3, false);
+  t3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, qhi), yhi, t3, false);
+  t4a = __builtin_amdgcn_udot2(qlo, qlo, t4a, false);
+  t4a = __builtin_amdgcn_udot2(qhi, qhi, t4a, false);
+}
+
+template <int LP, int NI>
+__global__ __launch_bounds__(256) void lyon8_u8_pow2(const uint8_t* __restrict__ prof,
+                                                     int64_t ps,
+                                                     const uint8_t* __restrict__ dm,
+                                                     int64_t ds, int64_t n,
+                                                     double* __restrict__ out) {
+  static_assert(NI == 8 || NI == 16, "ld = 8192 or 16384");
+  constexpr int PL = LP / 16;
+  constexpr int K = NI == 16 ? 14 : 13;  // ld = 2^K
+  constexpr int LD = 1 << K;
+  constexpr double SCALE = 1.0 / (double)(1ll << (2 * K));  // 2^-2K
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 7;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c < n; c += nwaves) {
+    const u32x4* drow = reinterpret_cast<const u32x4*>(dm + c * ds) + lane;
+    u32x4 q[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) q[i] = __builtin_nontemporal_load(drow + 64 * i);
+    const int pl = lane < PL ? lane : 0;
+    const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
+    // per instruction: this lane's 16 bytes' sum x and sum x^2; the row's y^3 / y^4 sums
+    uint32_t A[NI], B[NI];
+    uint32_t s1 = 0, s2 = 0;
+    int t3 = 0;
+    uint64_t t4 = 0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t a = __builtin_amdgcn_udot4(q[i].x, 0x01010101u, 0u, false);
+      a = __builtin_amdgcn_udot4(q[i].y, 0x01010101u, a, false);
+      a = __builtin_amdgcn_udot4(q[i].z, 0x01010101u, a, false);
+      a = __builtin_amdgcn_udot4(q[i].w, 0x01010101u, a, false);
+      uint32_t b = __builtin_amdgcn_udot4(q[i].x, q[i].x, 0u, false);
+      b = __builtin_amdgcn_udot4(q[i].y, q[i].y, b, false);
+      b = __builtin_amdgcn_udot4(q[i].z, q[i].z, b, false);
+      b = __builtin_amdgcn_udot4(q[i].w, q[i].w, b, false);
+      A[i] = a;
+      B[i] = b;
+      s1 += a;
+      s2 += b;
+      uint32_t u = 0, v = 0;  // each <= 2 dwords * 4 * 2^28 = 2^31
+      acc34_dword(q[i].x, t3, u);
+      acc34_dword(q[i].y, t3, u);
+      acc34_dword(q[i].z, t3, v);
+      acc34_dword(q[i].w, t3, v);
+      t4 += (uint64_t)u + (uint64_t)v;
+    }
+    Acc2 sp = {0, 0, 0, 0};
+    if (lane < PL) acc2_x4(pq, sp);
+    const long long S1 = wave_sum_i64((long long)s1);
+    const long long S2 = wave_sum_i64((long long)s2);
+    const long long T3 = wave_sum_i64((long long)t3);
+    const unsigned long long T4 = (unsigned long long)wave_sum_i64((long long)t4);
+    sp.s1 = (uint32_t)wave_sum_i64((long long)sp.s1);
+    sp.s2 = (uint32_t)wave_sum_i64((long long)sp.s2);
+    sp.t3 = (int)wave_sum_i64((long long)sp.t3);
+    sp.t4 = (uint64_t)wave_sum_i64((long long)sp.t4);
+    // ---- numpy's std of the DM row: exact leaf sums, numpy's tree above them
+    double ssq = 0.0;
+#pragma unroll
+    for (int s = 0; s < NI / 8; ++s) {
+      uint32_t va[8], vb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        va[k] = A[8 * s + k];
+        vb[k] = B[8 * s + k];
+      }
+      const long long la = reduce_scatter8(va, t), lb = reduce_scatter8(vb, t);
+      const long long v2k = (lb << (2 * K)) - ((2 * S1 * la) << K) + 128ll * S1 * S1;
+      const double chunk = leaf_tree64((double)v2k * SCALE);
+      ssq = s == 0 ? chunk : ssq + chunk;
+    }
+    // ---- finalise: lanes 0-3 the profile statistics, lanes 4-7 the DM row's
+    if (lane < 8) {
+      double v;
+      if (lane < 4) {
+        double st[4];
+        stats4<LP>(sp, st);
+        v = lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : st[3];
+      } else {
+        const double dn = (double)LD;
+        const long long T1 = S1 - 128ll * LD;
+        const long long T2 = S2 - 256ll * S1 + 16384ll * LD;
+        const Moments mo = moments_i128(LD, T1, T2, T3, T4);
+        const int k = lane - 4;
+        v = k == 0 ? (double)S1 / dn : k == 1 ? sqrt(ssq / dn) : stat_k(mo, k);
+      }
+      __builtin_nontemporal_store(v, out + c * 8 + lane);
+    }
+  }
+}
+
+// ---- long DM rows of 8192 + 2^j * M1 bytes: coalesced loads, leaves through LDS ---------
+// e.g. nDM = 120 (15 360 bytes: chunk 0 = 64 leaves of 128, chunk 1 = 64 leaves of 112).
+// The mean is not exact there, so numpy's leaf sums round and every d*d is added in numpy's
+// order as in lyon8_u8_long -- but the row is read with coalesced dwordx4 loads (16 B per
+// lane, 1 KiB per wave instruction, all issued up front) and each chunk is staged through a
+// wave-private LDS image, one leaf per lane, so a lane's 16 words come from LDS instead of 16
+// scattered global loads.
+//   * image: leaf l of a chunk at l * S, S = M + pad with S / 16 odd, so the ds_read_b128 of
+//     the 16 lanes of a bank group start on 16 distinct 16-B bank slots (conflict-free);
+//     M is a multiple of 16, so every 16-B piece lies in one leaf.
+//   * leaves of a chunk are a perfect pairwise tree in lane order (lanes past the last leaf
+//     hold 0), summed by wave_sum_f64's butterflies; the chunk sums are added in order.
+constexpr int L8_LDS_WAVE_BYTES = 64 * 144;  // 64 leaves at S <= 144
+
+// the LDS image is wave-private: order the wave's own stores and loads
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__host__ __device__ constexpr int lds_leaf_stride(int m) { return m + ((m / 16) % 2 == 0 ? 16 : 32); }
+
+template <int M>
+__device__ __forceinline__ double leaf_sumsq_lds(const uint8_t* img, int leaf, double mean) {
+  constexpr int S = lds_leaf_stride(M);
+  uint64_t w[16];
+  const u32x4* p = reinterpret_cast<const u32x4*>(img + leaf * S);
+#pragma unroll
+  for (int k = 0; k < M / 16; ++k) {
+    const u32x4 v = p[k];
+    w[2 * k] = ((uint64_t)v.y << 32) | v.x;
+    w[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+  return leaf_sumsq(w, M / 8, mean);
+}
+
+// write the chunk's pieces held in q[0..NP) (piece p = lane + 64 i, 16 B at chunk offset 16p)
+// into the image: leaf = 16p / M
+template <int M, int NP>
+__device__ __forceinline__ void stage_chunk(uint8_t* img, const u32x4 (&q)[NP], int lane, int len) {
+  constexpr int S = lds_leaf_stride(M);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int o = 16 * (lane + 64 * i);
+    if (o < len) {
+      const int leaf = o / M;  // M a compile-time constant: a multiply-shift
+      *reinterpret_cast<u32x4*>(img + leaf * S + (o - leaf * M)) = q[i];
+    }
+  }
+}
+
+template <int LP, int M1>
+__global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ prof, int64_t ps,
+                                                    const uint8_t* __restrict__ dm, int64_t ds,
+                                                    int64_t n, double* __restrict__ out, int ld) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][L8_LDS_WAVE_BYTES];
+  constexpr int PL = LP / 16;
+  const int lane = threadIdx.x & 63;
+  uint8_t* img = lds[threadIdx.x >> 6];
+  const int len1 = ld - 8192;                 // chunk 1: 2^j leaves of M1 bytes
+  const int leaves1 = len1 / M1;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c < n; c += nwaves) {
+    const u32x4* drow = reinterpret_cast<const u32x4*>(dm + c * ds);
+    u32x4 q0[8], q1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q0[i] = __builtin_nontemporal_load(drow + lane + 64 * i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // clamped: out-of-row pieces re-read the last one
+      const int p = lane + 64 * i;
+      q1[i] = __builtin_nontemporal_load(drow + 512 + (16 * p < len1 ? p : len1 / 16 - 1));
+    }
+    const int pl = lane < PL ? lane : 0;
+    const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
+    // ---- exact power sums (pieces past the row count as 0x80 bytes, removed below)
+    Acc2 sd = {0, 0, 0, 0};
+    int pad = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc2_x4(q0[i], sd);
+    stage_chunk<128>(img, q0, lane, 8192);  // chunk 0's image (q0 dies here)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool in = 16 * (lane + 64 * i) < len1;
+      const u32x4 h = (u32x4){0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+      acc2_x4(in ? q1[i] : h, sd);
+      pad += in ? 0 : 16;
+    }
+    Acc2 sp = {0, 0, 0, 0};
+    if (lane < PL) acc2_x4(pq, sp);
+    const long long S1 = wave_sum_i64((long long)sd.s1 - 128ll * pad);
+    const long long S2 = wave_sum_i64((long long)sd.s2 - 16384ll * pad);
+    const long long T3 = wave_sum_i64((long long)sd.t3);
+    const unsigned long long T4 = (unsigned long long)wave_sum_i64((long long)sd.t4);
+    sp.s1 = (uint32_t)wave_sum_i64((long long)sp.s1);
+    sp.s2 = (uint32_t)wave_sum_i64((long long)sp.s2);
+    sp.t3 = (int)wave_sum_i64((long long)sp.t3);
+    sp.t4 = (uint64_t)wave_sum_i64((long long)sp.t4);
+    const double dn = (double)ld;
+    const double mean = (double)S1 / dn;
+    // ---- numpy's std: chunk 0 (64 leaves of 128), then chunk 1, each staged through LDS
+    wave_lds_sync();
+    const double c0 = wave_sum_f64(leaf_sumsq_lds<128>(img, lane, mean));
+    wave_lds_sync();
+    stage_chunk<M1>(img, q1, lane, len1);
+    wave_lds_sync();
+    const double c1 = wave_sum_f64(lane < leaves1 ? leaf_sumsq_lds<M1>(img, lane, mean) : 0.0);
+    wave_lds_sync();
+    const double ssq = c0 + c1;
+    if (lane < 8) {
+      double v;
+      if (lane < 4) {
+        double st[4];
+        stats4<LP>(sp, st);
+        v = lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : st[3];
+      } else {
+        const long long T1 = S1 - 128ll * ld;
+        const long long T2 = S2 - 256ll * S1 + 16384ll * ld;
+        const Moments mo = moments_i128(ld, T1, T2, T3, T4);
+        const int k = lane - 4;
+        v = k == 0 ? mean : k == 1 ? sqrt(ssq / dn) : stat_k(mo, k);
+      }
+      __builtin_nontemporal_store(v, out + c * 8 + lane);
+    }
+  }
+}
+
 // ---- fp64 rows (PFD) -------------------------------------------------------------------
 // Two-pass fp64, as numpy/scipy: mean = sum/n; m_k = mean((x-mean)^k) with d^3 = d^2*d and
 // d^4 = (d^2)^2 (scipy.stats._moment exponentiation by squares).  One wave per row.
@@ -534,6 +837,53 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
       PFE_L8U(256);
 #undef PFE_L8U
 #undef PFE_L8
+  } else if (aligned && (lp == 64 || lp == 128 || lp == 256) && (ld == 8192 || ld == 16384)) {
+    // nDM = 64 / 128 DataBlock rows: exact leaf sums, coalesced loads (lyon8_u8_pow2)
+    const int grid = grid_for(n, o.lyon8_blocks);
+#define PFE_L8P(LL, NN) \
+  hipLaunchKernelGGL((lyon8_u8_pow2<LL, NN>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out)
+    if (ld == 16384) {
+      if (lp == 64)
+        PFE_L8P(64, 16);
+      else if (lp == 128)
+        PFE_L8P(128, 16);
+      else
+        PFE_L8P(256, 16);
+    } else {
+      if (lp == 64)
+        PFE_L8P(64, 8);
+      else if (lp == 128)
+        PFE_L8P(128, 8);
+      else
+        PFE_L8P(256, 8);
+    }
+#undef PFE_L8P
+  } else if (int m1 = 0, l1 = 0; aligned && (lp == 64 || lp == 128 || lp == 256) && ld > 8192 &&
+                                  ld < 16384 && ld % 16 == 0 && perfect_chunk(ld - 8192, m1, l1) &&
+                                  m1 % 16 == 0) {
+    // 8192 + 2^j * M1 bytes (nDM = 120: 15 360): coalesced loads, leaves through LDS
+    const int grid = grid_for(n, o.lyon8_blocks);
+#define PFE_L8S(LL, MM) \
+  hipLaunchKernelGGL((lyon8_u8_lds<LL, MM>), dim3(grid), dim3(256), 0, st, prof, ps, dm, ds, n, out, ld)
+#define PFE_L8SM(LL)          \
+  do {                        \
+    if (m1 == 80)             \
+      PFE_L8S(LL, 80);        \
+    else if (m1 == 96)        \
+      PFE_L8S(LL, 96);        \
+    else if (m1 == 112)       \
+      PFE_L8S(LL, 112);       \
+    else                      \
+      PFE_L8S(LL, 128);       \
+  } while (0)
+    if (lp == 64)
+      PFE_L8SM(64);
+    else if (lp == 128)
+      PFE_L8SM(128);
+    else
+      PFE_L8SM(256);
+#undef PFE_L8SM
+#undef PFE_L8S
   } else if (LongShape sh{}; aligned && (lp == 64 || lp == 128 || lp == 256) &&
                                 long_row_shape(ld, sh)) {
     // real PHCX shape: short profile + the whole DataBlock (lyon8_u8_long)

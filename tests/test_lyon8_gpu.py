@@ -94,10 +94,14 @@ def test_large_batch_properties(engine):
 
 
 @pytest.mark.parametrize("lp,ld", [(128, 15360), (128, 16384), (64, 7680), (256, 8192),
-                                   (128, 12800), (128, 8320), (64, 384), (256, 10240)])
+                                   (128, 12800), (128, 8320), (64, 384), (256, 10240),
+                                   (64, 16384), (256, 16384), (128, 8192), (64, 8192),
+                                   (64, 14336), (256, 13312), (128, 12288)])
 def test_long_dm_rows_vs_oracle(engine, lp, ld):
-    """The real PHCX shape (lyon8_u8_long): a 64-256-bin profile and the whole section-0
-    DataBlock (nDM x 128 bytes; nDM = 120, 128, 60, 64, 100, 65, 3, 80).  mean and std
+    """The real PHCX shape: a 64-256-bin profile and the whole section-0 DataBlock (nDM x
+    128 bytes; nDM = 120, 128, 60, 64, 100, 65, 3, 80, 112, 104, 96).  Kernels: nDM = 64 / 128
+    lyon8_u8_pow2 (exact leaf sums); 8192 + 2^j * {80, 96, 112, 128} bytes (nDM = 65, 80, 96,
+    104, 112, 120) lyon8_u8_lds; the rest lyon8_u8_long.  mean and std
     bit-exact for both rows -- the DM row's std follows numpy's own reduction (8192-element
     chunks, each a pairwise tree) -- skew/kurt within 1e-12."""
     prof, dm = lyon_batch(300, lp, ld, seed=31 + ld, adversarial=True)
