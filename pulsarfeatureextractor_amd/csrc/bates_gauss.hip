@@ -56,3 +56,5 @@ hipError_t launch_gauss(const BatesArgs& a, hipStream_t st) {
 }
 
 }  // namespace pfe
+
+PFE_LM_PROFILE_EXPORT(gauss)

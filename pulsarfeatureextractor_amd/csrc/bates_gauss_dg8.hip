@@ -33,3 +33,5 @@ hipError_t launch_gauss_dg8(const BatesArgs& a, hipStream_t st) {
 }
 
 }  // namespace pfe
+
+PFE_LM_PROFILE_EXPORT(gauss_dg8)

@@ -40,3 +40,5 @@ hipError_t launch_gauss_peel(const BatesArgs& a, hipStream_t st) {
 }
 
 }  // namespace pfe
+
+PFE_LM_PROFILE_EXPORT(gauss_peel)

@@ -108,6 +108,10 @@ def main():
     pfd = "--pfd" in sys.argv
     src = [a for a in sys.argv[1:] if not a.startswith("--")][0]
     prof = json.load(open(src))
+    # the Gaussian chain is three translation units, each with its own counter set
+    for k in list(prof):
+        if k.startswith(("gauss_peel/", "gauss_dg8/")):
+            prof.setdefault("gauss/" + k.split("/", 1)[1], prof[k])
     hp, hd = mean_hist_bins_pfd() if pfd else mean_hist_bins()
     n_cand = prof["gauss/N=8"]["calls"]
     total = 0.0
