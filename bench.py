@@ -865,8 +865,9 @@ def main():
                 ctx.eng.pfd_bates22(tp, tf, ts, out=out, status=status)
 
             elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
+            # 0 (no frozen count for this fold shape): no roofline fraction, never the PHCX count
             ops = (load_ops_per_candidate("r03_pfd22_ops.json")
-                   if pfd_shape == (16, 32, 128) else None)
+                   if pfd_shape == (16, 32, 128) else None) or 0
             roof = bates_roofline(n, kern_ms, kern_max, "pfe_pfd_bates22 (9 kernels, one step)",
                                   ops=ops)
             roof["note"] = ("algorithmic fp64 operations of PFDFile.compute on 16x32x128 folds "

@@ -39,7 +39,8 @@ def main():
     eng = _native.Engine(0)
     if args.solver:
         eng.set_option("solver", args.solver)
-    tags = ("gauss", "gauss_peel", "gauss_dg8", "sine_dm_sub")  # one counter set per translation unit + (("pfd22",) if args.path == "pfd22" else ())
+    # one counter set per translation unit
+    tags = ("gauss", "gauss_peel", "gauss_dg8", "sine_dm_sub") + (("pfd22",) if args.path == "pfd22" else ())
     buf = (C.c_ulonglong * 64)()
     import time
     if args.path == "bates22":
