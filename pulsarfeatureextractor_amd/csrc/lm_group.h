@@ -143,9 +143,12 @@ __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
 }
 
 // qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%G, slot r/G)
+// rajjv[j] = 1 / a[j][j] of step j's Householder vector (0 for a zero column): the divisor
+// Q^T f divides by in glm_outer, so the contracted build takes it from here instead of a
+// second division
 template <int N, int MPL, int G = GLM_G>
 __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
-                                        double (&acnorm)[N]) {
+                                        double (&acnorm)[N], double (&rajjv)[N]) {
   PFE_LA_CONTRACT
   static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
   const int gl = glane<G>();
@@ -201,6 +204,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
     for (int k = 0; k < MPL; ++k)
       if (row_ge(gl, k, j)) p += a[k][j] * a[k][j];
     double ajnorm = sqrt(gsum<G>(p));
+    rajjv[j] = 0.0;
     if (ajnorm != 0.0) {
       if (gbcast<G>(a[0][j], j) < 0.0) ajnorm = -ajnorm;
       const double rinv = 1.0 / ajnorm;
@@ -222,6 +226,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       gsum_from<N, G>(d, j + 1);
       const double ajj = gbcast<G>(a[0][j], j);
       const double rajj = 1.0 / ajj;
+      rajjv[j] = rajj;
 #pragma unroll
       for (int c = j + 1; c < N; ++c) {
         const double temp = la_quot(d[c], ajj, rajj);
@@ -229,8 +234,13 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
         if (rdiag[c] != 0.0) {
-          const double t2 = gbcast<G>(a[0][c], j) / rdiag[c];
-          rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
+          const double ajc = gbcast<G>(a[0][c], j);
+          if (LA_EXACT_QUOTIENTS) {
+            const double t2 = ajc / rdiag[c];
+            rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
+          } else {  // rdiag sqrt(1 - (ajc/rdiag)^2) without the quotient
+            rdiag[c] = sqrt(fmax(0.0, (rdiag[c] - ajc) * (rdiag[c] + ajc)));
+          }
           if (la_norm_lost(rdiag[c], wa[c])) {
             double r = 0.0;
 #pragma unroll
@@ -326,8 +336,8 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   }
   nfev += N;
   int ipvt[N];
-  double rdiag[N], acn[N];
-  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn);
+  double rdiag[N], acn[N], rajjv[N];
+  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn, rajjv);
   double diag[N];
   double xnorm = 0.0, delta = 0.0;
   if (iter == 1) {
@@ -360,7 +370,7 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) p += fjac[k][j] * wa4[k];
       const double sum = gsum<G>(p);
-      const double temp = -sum / ajj;
+      const double temp = la_quot(-sum, ajj, rajjv[j]);
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) wa4[k] = wa4[k] + fjac[k][j] * temp;
