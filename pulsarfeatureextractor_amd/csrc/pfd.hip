@@ -160,21 +160,36 @@ __device__ __forceinline__ double filter_neg_pfd(double v) {
   return (fabs(v - 0.0) > 0.000005 && v < 0.0) ? 0.0 : v;
 }
 
-// numpy.argmax of an LDS row: the first maximum, or the first NaN
-__device__ int np_argmax_seq(const double* a, int n, int shift, double sub) {
-  auto at = [&](int i) { int j = i + shift; j %= n; if (j < 0) j += n; return a[j] - sub; };
-  int bi = 0;
-  double bv = at(0);
-  if (!(bv == bv)) return 0;
-  for (int i = 1; i < n; ++i) {
-    const double v = at(i);
-    if (!(v == v)) return i;
-    if (v > bv) {
+// numpy.argmax over i of a[(i + shift) mod n] - sub (|shift| < n) as a wave reduction: the
+// first NaN if there is one, else the first maximum (the values are the same roundings a
+// sequential scan compares; ties go to the smaller i, so +0 / -0 ties too)
+__device__ int np_argmax_wave(const double* a, int n, int shift, double sub, int lane) {
+  int nan_i = 1 << 30, bi = 1 << 30;
+  double bv = 0.0;
+  for (int i = lane; i < n; i += 64) {
+    int j = i + shift;
+    if (j >= n) j -= n;
+    if (j < 0) j += n;
+    const double v = a[j] - sub;
+    if (!(v == v)) {
+      if (i < nan_i) nan_i = i;
+    } else if (bi == (1 << 30) || v > bv) {
       bv = v;
       bi = i;
     }
   }
-  return bi;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const int on = __shfl_xor(nan_i, m);
+    const double ov = __shfl_xor(bv, m);
+    const int oi = __shfl_xor(bi, m);
+    nan_i = on < nan_i ? on : nan_i;
+    if (oi != (1 << 30) && (bi == (1 << 30) || ov > bv || (ov == bv && oi < bi))) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  return nan_i != (1 << 30) ? nan_i : (bi != (1 << 30) ? bi : 0);
 }
 
 // PFDOperations.getCandidateParameters (PFDOperations.py:130-231): the S/N of the profile
@@ -185,13 +200,13 @@ __device__ int np_argmax_seq(const double* a, int n, int shift, double sub) {
 // that of the half maximum.
 __device__ void pfd_params(const double* prof, double* tmp, int L, int lane, double& snr,
                            double& width) {
-  const double avg = np_pairwise<12>(prof, L, lane) / (double)L;          // :130
+  const double avg = np_sum_row(prof, L, lane) / (double)L;          // :130
   for (int b = lane; b < L; b += 64) {
     const double d = prof[b] - avg;
     tmp[b] = d * d;
   }
   lds_sync();
-  const double var = np_pairwise<12>(tmp, L, lane) / (double)L;          // :131
+  const double var = np_sum_row(tmp, L, lane) / (double)L;          // :131
   lds_sync();
   const double sigma = sqrt(var);
   const double lo = avg - 3.0 * sigma, hi = avg + 3.0 * sigma;
@@ -204,40 +219,50 @@ __device__ void pfd_params(const double* prof, double* tmp, int L, int lane, dou
     m += __popcll(bal);
   }
   lds_sync();
-  const double avg2 = np_pairwise<12>(tmp, m, lane) / (double)m;         // :148 (empty: NaN)
+  const double avg2 = np_sum_row(tmp, m, lane) / (double)m;         // :148 (empty: NaN)
   lds_sync();
   for (int i = lane; i < m; i += 64) {
     const double d = tmp[i] - avg2;
     tmp[i] = d * d;
   }
   lds_sync();
-  const double var2 = np_pairwise<12>(tmp, m, lane) / (double)m;         // :149
+  const double var2 = np_sum_row(tmp, m, lane) / (double)m;         // :149
   lds_sync();
   const double sd2 = sqrt(var2);
   for (int b = lane; b < L; b += 64) tmp[b] = (prof[b] - avg2) / sd2;
   lds_sync();
-  snr = np_pairwise<12>(tmp, L, lane);                                    // :151
+  snr = np_sum_row(tmp, L, lane);                                    // :151
   lds_sync();
   if (snr < 0.0) snr = 0.1;                                              // :152-153
-  // width (:194-231), every lane walking the LDS row identically
-  const int peak0 = np_argmax_seq(prof, L, 0, 0.0);
+  // width (:194-231): the sequential scans of the reference as wave reductions over the
+  // same values (the rotated profile minus its Python min)
+  const int peak0 = np_argmax_wave(prof, L, 0, 0.0, lane);
   const int shift = peak0 - L / 2;                                        // Py2 int '/'
-  const double pmin = py_min_seq(prof, L);
-  auto rot = [&](int i) { int j = (i + shift) % L; if (j < 0) j += L; return prof[j] - pmin; };
-  const int peak = np_argmax_seq(prof, L, shift, pmin);
-  double rmax = rot(0);
-  for (int i = 1; i < L; ++i)
-    if (rot(i) > rmax) rmax = rot(i);
+  const double pmin = py_ext_wave<false>(prof, L, lane);
+  auto rot = [&](int i) { int j = i + shift; if (j >= L) j -= L; if (j < 0) j += L; return prof[j] - pmin; };
+  const int peak = np_argmax_wave(prof, L, shift, pmin, lane);
+  // rmax: rot(0), raised by every later rot(i) > rmax -- NaN when rot(0) is, else the
+  // largest non-NaN value (fmax skips NaN)
+  const double r0 = rot(0);
+  double rm = r0;
+  for (int i = lane; i < L; i += 64) rm = fmax(rm, rot(i));
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) rm = fmax(rm, __shfl_xor(rm, m));
+  const double rmax = (r0 == r0) ? rm : r0;
   const double half = rmax / 2.0;
-  int left = peak;
-  while (left > 0) {
-    if (rot(left) < half) break;
-    --left;
+  // left: the largest l in [1, peak] with rot(l) < half, else 0; right: the smallest r in
+  // [peak, L) with rot(r) < half, else L (where the reference's walks stop)
+  int left = 0, right = L;
+  for (int i = lane; i < L; i += 64) {
+    const bool below = rot(i) < half;
+    if (below && i >= 1 && i <= peak && i > left) left = i;
+    if (below && i >= peak && i < right) right = i;
   }
-  int right = peak;
-  while (right < L) {
-    if (rot(right) < half) break;
-    ++right;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const int ol = __shfl_xor(left, m), orr = __shfl_xor(right, m);
+    left = ol > left ? ol : left;
+    right = orr < right ? orr : right;
   }
   width = (1.0 * ((double)(right - left) - 1.0)) / (double)L;           // :231
 }
@@ -267,7 +292,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
                                    double* bmean, double* bvar, int NS, int L, int lane,
                                    double width, double (&o)[3]) {
   // s22 first, while T holds the sub-band profiles
-  const double pm = np_pairwise<12>(prof, L, lane) / (double)L;
+  const double pm = np_sum_row(prof, L, lane) / (double)L;
   for (int b = lane; b < L; b += 64) tmp[b] = prof[b] - pm;
   lds_sync();
   const double inv2 = 1.0 / (double)(L - 1);
@@ -275,9 +300,15 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   double integ = 0.0;
   for (int j = 0; j < NS; ++j) {
     const double* r = T + (size_t)j * L;
-    const double mj = np_pairwise<12>(r, L, lane) / (double)L;
-    const double d = wdot(L, lane, [&](int b) { return (r[b] - mj) * tmp[b]; });
-    const double q = wdot(L, lane, [&](int b) { return (r[b] - mj) * (r[b] - mj); });
+    const double mj = np_sum_row(r, L, lane) / (double)L;
+    double dl_ = 0.0, ql_ = 0.0;  // wdot's order for both sums, in one pass
+    for (int b = lane; b < L; b += 64) {
+      const double e = r[b] - mj;
+      dl_ += e * tmp[b];
+      ql_ += e * e;
+    }
+    const double d = wsum(dl_);
+    const double q = wsum(ql_);
     const double cc = fabs(corr_pfd(d * inv2, q * inv2, pvar * inv2));
     if (cc > 0.0055) integ += cc;                                      // :463-464, :437-439
   }
@@ -291,8 +322,16 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   for (int i = 0; i < NS; ++i) {
     double* r = T + (size_t)i * L;
     for (int j = lane; j < nw; j += 64) {
-      double s = 0.0;
-      for (int b = 0; b < wb; ++b) s += r[j + b];
+      double s = 0.0;  // r[j] + r[j+1] + ... in order; loads issued 8 at a time
+      int b = 0;
+      for (; b + 8 <= wb; b += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = r[j + b + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+      }
+      for (; b < wb; ++b) s += r[j + b];
       tmp[j] = s;
     }
     lds_sync();
@@ -324,7 +363,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
     lds_sync();
   }
   // RMS scatter of the maxima (:1629-1651)
-  const double med = np_pairwise<12>(mb, NS, lane) / (double)NS;
+  const double med = np_sum_row(mb, NS, lane) / (double)NS;
   int count = 0;
   double var_med = 0.0;
   for (int i = 0; i < NS; ++i)
@@ -347,7 +386,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   // mean pairwise correlation of the boxcar sums, pairs (i < k) in order (:1653-1677)
   for (int i = 0; i < NS; ++i) {
     double* r = T + (size_t)i * L;
-    const double m = np_pairwise<12>(r, nw, lane) / (double)nw;
+    const double m = np_sum_row(r, nw, lane) / (double)nw;
     lds_sync();
     for (int j = lane; j < nw; j += 64) r[j] = r[j] - m;
     lds_sync();
@@ -355,20 +394,37 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
     if (lane == 0) bvar[i] = v;
   }
   lds_sync();
+  // one pair per lane at a time: the lane's dot product runs over j sequentially from a
+  // lane-dependent start (the 64 lanes' LDS reads of one step then spread over the banks),
+  // and the pairs' correlations are summed as a wave reduction (s21 is held to 1e-12: numpy's
+  // own dots run in BLAS order)
   const double inv = 1.0 / (double)(nw - 1);
-  double csum = 0.0;
-  int m = 0;
-  for (int i = 0; i < NS; ++i)
-    for (int k = i + 1; k < NS; ++k) {
-      const double* ri = T + (size_t)i * L;
-      const double* rk = T + (size_t)k * L;
-      const double d = wdot(nw, lane, [&](int j) { return ri[j] * rk[j]; });
-      const double cc = corr_pfd(d * inv, bvar[i] * inv, bvar[k] * inv);
-      if (cc == cc) {
-        csum += cc;
-        ++m;
-      }
+  double csum_l = 0.0;
+  int m_l = 0;
+  const int npairs = NS * (NS - 1) / 2;
+  for (int p = lane; p < npairs; p += 64) {
+    int i = 0, rem = p;
+    while (rem >= NS - 1 - i) {
+      rem -= NS - 1 - i;
+      ++i;
     }
+    const int k = i + 1 + rem;
+    const double* ri = T + (size_t)i * L;
+    const double* rk = T + (size_t)k * L;
+    int j = lane % nw;
+    double d = 0.0;
+    for (int t = 0; t < nw; ++t) {
+      d += ri[j] * rk[j];
+      j = (j + 1 == nw) ? 0 : j + 1;
+    }
+    const double cc = corr_pfd(d * inv, bvar[i] * inv, bvar[k] * inv);
+    if (cc == cc) {
+      csum_l += cc;
+      ++m_l;
+    }
+  }
+  const double csum = wsum(csum_l);
+  const int m = wsum_i(m_l);
   if (m == 0) return false;                                             // ZeroDivisionError
   o[0] = rms;
   o[1] = csum / (double)m;
