@@ -283,6 +283,33 @@ __device__ __forceinline__ double wdot(int n, int lane, Fn f) {
   return wsum(s);
 }
 
+// numpy's leaf sum (8 <= n <= 128) of eight rows at once: row g = lane / 8 in lanes
+// 8g..8g+7, accumulator t = lane & 7 (its loads issued before its adds), combined
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by DPP inside the 8 lanes, then the remainder in
+// order: np_leaf's additions, so np_leaf's bits, in every lane of the group
+__device__ __forceinline__ double np_leaf_rows8(const double* row, int n, int t) {
+  const int nb = n - (n % 8);
+  double v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = row[min(t + 8 * m, n - 1)];
+  double r = v[0];
+#pragma unroll
+  for (int m = 1; m < 16; ++m)
+    if (8 * m < nb) r += v[m];
+  r += dpp_f64<DPP_QUAD_XOR1>(r);
+  r += dpp_f64<DPP_QUAD_XOR2>(r);
+  r += dpp_f64<DPP_ROW_HALF_MIRROR>(r);
+  for (int i = nb; i < n; ++i) r += row[i];
+  return r;
+}
+// sum over the 8 lanes of a group (the per-band dots of s21 / s22, held to 1e-12)
+__device__ __forceinline__ double sum8(double v) {
+  v += dpp_f64<DPP_QUAD_XOR1>(v);
+  v += dpp_f64<DPP_QUAD_XOR2>(v);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  return v;
+}
+
 // PFDOperations.getSubbandParameters (PFDOperations.py:401-441): s20 / s21 from
 // ProfileOperations.getSubband_scores (ProfileOperations.py:1585-1686) over the dedispersed
 // sub-band profiles T (nsub x L, profs.sum(0), PFDFile.plot_subbands :442-456) and s22 from
@@ -298,19 +325,42 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   const double inv2 = 1.0 / (double)(L - 1);
   const double pvar = wdot(L, lane, [&](int b) { return tmp[b] * tmp[b]; });
   double integ = 0.0;
-  for (int j = 0; j < NS; ++j) {
-    const double* r = T + (size_t)j * L;
-    const double mj = np_sum_row(r, L, lane) / (double)L;
-    double dl_ = 0.0, ql_ = 0.0;  // wdot's order for both sums, in one pass
-    for (int b = lane; b < L; b += 64) {
-      const double e = r[b] - mj;
-      dl_ += e * tmp[b];
-      ql_ += e * e;
+  const bool rows8 = L >= 8 && L <= 128;
+  if (rows8) {
+    // eight bands per step (band j0 + lane / 8); the |cc| of each band in bvar, then summed
+    // in band order
+    const int g = lane >> 3, t = lane & 7;
+    for (int j0 = 0; j0 < NS; j0 += 8) {
+      const int j = min(j0 + g, NS - 1);
+      const double* r = T + (size_t)j * L;
+      const double mj = np_leaf_rows8(r, L, t) / (double)L;
+      double dl_ = 0.0, ql_ = 0.0;
+      for (int b = t; b < L; b += 8) {
+        const double e = r[b] - mj;
+        dl_ += e * tmp[b];
+        ql_ += e * e;
+      }
+      const double d = sum8(dl_), q = sum8(ql_);
+      if (t == 0 && j0 + g < NS) bvar[j] = fabs(corr_pfd(d * inv2, q * inv2, pvar * inv2));
     }
-    const double d = wsum(dl_);
-    const double q = wsum(ql_);
-    const double cc = fabs(corr_pfd(d * inv2, q * inv2, pvar * inv2));
-    if (cc > 0.0055) integ += cc;                                      // :463-464, :437-439
+    lds_sync();
+    for (int j = 0; j < NS; ++j)
+      if (bvar[j] > 0.0055) integ += bvar[j];                          // :463-464, :437-439
+  } else {
+    for (int j = 0; j < NS; ++j) {
+      const double* r = T + (size_t)j * L;
+      const double mj = np_sum_row(r, L, lane) / (double)L;
+      double dl_ = 0.0, ql_ = 0.0;  // wdot's order for both sums, in one pass
+      for (int b = lane; b < L; b += 64) {
+        const double e = r[b] - mj;
+        dl_ += e * tmp[b];
+        ql_ += e * e;
+      }
+      const double d = wsum(dl_);
+      const double q = wsum(ql_);
+      const double cc = fabs(corr_pfd(d * inv2, q * inv2, pvar * inv2));
+      if (cc > 0.0055) integ += cc;                                    // :463-464, :437-439
+    }
   }
   lds_sync();
   const int wb = (int)ceil(width * (double)L);                          // :1603
@@ -384,14 +434,36 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   }
   const double rms = sqrt(var) / (double)wb;
   // mean pairwise correlation of the boxcar sums, pairs (i < k) in order (:1653-1677)
-  for (int i = 0; i < NS; ++i) {
-    double* r = T + (size_t)i * L;
-    const double m = np_sum_row(r, nw, lane) / (double)nw;
-    lds_sync();
-    for (int j = lane; j < nw; j += 64) r[j] = r[j] - m;
-    lds_sync();
-    const double v = wdot(nw, lane, [&](int j) { return r[j] * r[j]; });
-    if (lane == 0) bvar[i] = v;
+  if (rows8 && nw >= 8) {
+    // eight bands per step: numpy's mean of the boxcar row, centred in place by the lanes
+    // that own the elements (j = t mod 8), then the sum of squares
+    const int g = lane >> 3, t = lane & 7;
+    for (int i0 = 0; i0 < NS; i0 += 8) {
+      const int i = i0 + g;
+      const bool own = i < NS;
+      double* r = T + (size_t)(own ? i : NS - 1) * L;
+      const double m = np_leaf_rows8(r, nw, t) / (double)nw;
+      lds_sync();
+      double v = 0.0;
+      for (int j = t; j < nw; j += 8) {
+        const double c = r[j] - m;
+        if (own) r[j] = c;
+        v += c * c;
+      }
+      v = sum8(v);
+      if (own && t == 0) bvar[i] = v;
+      lds_sync();
+    }
+  } else {
+    for (int i = 0; i < NS; ++i) {
+      double* r = T + (size_t)i * L;
+      const double m = np_sum_row(r, nw, lane) / (double)nw;
+      lds_sync();
+      for (int j = lane; j < nw; j += 64) r[j] = r[j] - m;
+      lds_sync();
+      const double v = wdot(nw, lane, [&](int j) { return r[j] * r[j]; });
+      if (lane == 0) bvar[i] = v;
+    }
   }
   lds_sync();
   // one pair per lane at a time: the lane's dot product runs over j sequentially from a
