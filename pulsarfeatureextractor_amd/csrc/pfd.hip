@@ -369,7 +369,72 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   // boxcar sums, a Python loop per window (:1608-1617), in place of each band's row
   bool have = false;
   double last_mb = 0.0;
-  for (int i = 0; i < NS; ++i) {
+  if (rows8) {
+    // eight bands per step (band i0 + lane / 8, windows j = t mod 8 in registers until every
+    // lane has read the row): the same sums in the same order; each band's first strict
+    // maximum above -10000.0 by an 8-lane (value, first index) reduction; bmean holds the
+    // band's max_bin or -1 (none), resolved in band order below
+    const int g = lane >> 3, t = lane & 7;
+    for (int i0 = 0; i0 < NS; i0 += 8) {
+      const int i = i0 + g;
+      const bool own = i < NS;
+      double* r = T + (size_t)(own ? i : NS - 1) * L;
+      double sv[16];
+      double bvv = -10000.0;
+      int bj = 1 << 30;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = t + 8 * q;
+        double sm = 0.0;
+        if (j < nw) {
+          int b = 0;
+          for (; b + 8 <= wb; b += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = r[j + b + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sm += v[u];
+          }
+          for (; b < wb; ++b) sm += r[j + b];
+          if (sm > bvv) {
+            bvv = sm;
+            bj = j;
+          }
+        }
+        sv[q] = sm;
+      }
+      {
+        double ov = dpp_f64<DPP_QUAD_XOR1>(bvv);
+        int oj = dpp_i32<DPP_QUAD_XOR1>(bj);
+        if (ov > bvv || (ov == bvv && oj < bj)) { bvv = ov; bj = oj; }
+        ov = dpp_f64<DPP_QUAD_XOR2>(bvv);
+        oj = dpp_i32<DPP_QUAD_XOR2>(bj);
+        if (ov > bvv || (ov == bvv && oj < bj)) { bvv = ov; bj = oj; }
+        ov = dpp_f64<DPP_ROW_HALF_MIRROR>(bvv);
+        oj = dpp_i32<DPP_ROW_HALF_MIRROR>(bj);
+        if (ov > bvv || (ov == bvv && oj < bj)) { bvv = ov; bj = oj; }
+      }
+      if (own && t == 0) bmean[i] = bj < (1 << 30) ? (double)(bj + wb / 2) : -1.0;  // Py2 wb/2
+      lds_sync();
+      if (own) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (t + 8 * q < nw) r[t + 8 * q] = sv[q];
+      }
+      lds_sync();
+    }
+    for (int i = 0; i < NS; ++i) {  // max_bin is one local across the bands
+      const double v = bmean[i];
+      if (v >= 0.0) {
+        have = true;
+        last_mb = v;
+      }
+      if (!have) return false;
+      if (lane == 0) mb[i] = last_mb;
+    }
+    lds_sync();
+  }
+  for (int i = 0; !rows8 && i < NS; ++i) {
     double* r = T + (size_t)i * L;
     for (int j = lane; j < nw; j += 64) {
       double s = 0.0;  // r[j] + r[j+1] + ... in order; loads issued 8 at a time
@@ -501,7 +566,6 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   o[0] = rms;
   o[1] = csum / (double)m;
   o[2] = integ;
-  (void)bmean;
   return true;
 }
 
