@@ -369,6 +369,11 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   // boxcar sums, a Python loop per window (:1608-1617), in place of each band's row
   bool have = false;
   double last_mb = 0.0;
+  // packed: the boxcar rows are stored at an odd stride RS <= L (rows rewritten in band order
+  // never reach a row not yet read), so the pair loop's lanes, all at the same j of different
+  // rows, read distinct LDS banks
+  const bool packed = rows8 && nw >= 8 && (nw | 1) <= L;
+  const int RS = packed ? (nw | 1) : L;
   if (rows8) {
     // eight bands per step (band i0 + lane / 8, windows j = t mod 8 in registers until every
     // lane has read the row): the same sums in the same order; each band's first strict
@@ -417,9 +422,10 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
       if (own && t == 0) bmean[i] = bj < (1 << 30) ? (double)(bj + wb / 2) : -1.0;  // Py2 wb/2
       lds_sync();
       if (own) {
+        double* w = T + (size_t)i * RS;
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          if (t + 8 * q < nw) r[t + 8 * q] = sv[q];
+          if (t + 8 * q < nw) w[t + 8 * q] = sv[q];
       }
       lds_sync();
     }
@@ -506,7 +512,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
     for (int i0 = 0; i0 < NS; i0 += 8) {
       const int i = i0 + g;
       const bool own = i < NS;
-      double* r = T + (size_t)(own ? i : NS - 1) * L;
+      double* r = T + (size_t)(own ? i : NS - 1) * RS;
       const double m = np_leaf_rows8(r, nw, t) / (double)nw;
       lds_sync();
       double v = 0.0;
@@ -531,9 +537,9 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
     }
   }
   lds_sync();
-  // one pair per lane at a time: the lane's dot product runs over j sequentially from a
-  // lane-dependent start (the 64 lanes' LDS reads of one step then spread over the banks),
-  // and the pairs' correlations are summed as a wave reduction (s21 is held to 1e-12: numpy's
+  // one pair per lane at a time (rows at the odd stride RS, or from a lane-dependent start
+  // when not packed, so the 64 lanes' LDS reads of one step spread over the banks), and the
+  // pairs' correlations are summed as a wave reduction (s21 is held to 1e-12: numpy's
   // own dots run in BLAS order)
   const double inv = 1.0 / (double)(nw - 1);
   double csum_l = 0.0;
@@ -546,13 +552,28 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
       ++i;
     }
     const int k = i + 1 + rem;
-    const double* ri = T + (size_t)i * L;
-    const double* rk = T + (size_t)k * L;
-    int j = lane % nw;
+    const double* ri = T + (size_t)i * RS;
+    const double* rk = T + (size_t)k * RS;
     double d = 0.0;
-    for (int t = 0; t < nw; ++t) {
-      d += ri[j] * rk[j];
-      j = (j + 1 == nw) ? 0 : j + 1;
+    if (packed) {  // every lane at the same j: four chains, loads first
+      double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+      int j = 0;
+      for (; j + 4 <= nw; j += 4) {
+        const double a0 = ri[j], a1 = ri[j + 1], a2 = ri[j + 2], a3 = ri[j + 3];
+        const double b0 = rk[j], b1 = rk[j + 1], b2 = rk[j + 2], b3 = rk[j + 3];
+        d0 += a0 * b0;
+        d1 += a1 * b1;
+        d2 += a2 * b2;
+        d3 += a3 * b3;
+      }
+      for (; j < nw; ++j) d0 += ri[j] * rk[j];
+      d = (d0 + d1) + (d2 + d3);
+    } else {
+      int j = lane % nw;
+      for (int t = 0; t < nw; ++t) {
+        d += ri[j] * rk[j];
+        j = (j + 1 == nw) ? 0 : j + 1;
+      }
     }
     const double cc = corr_pfd(d * inv, bvar[i] * inv, bvar[k] * inv);
     if (cc == cc) {
