@@ -621,6 +621,8 @@ def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2)
     elapsed, kern_ms, kern_max = ctx.time_steps(step, steps, warmup)
     per_cand = lp + ld + 8 * 8
     achieved = per_cand * n / (kern_ms * 1e-3) / 1e9
+    # HBM bytes per launch from the committed PMC passes of the same shape (tools/summarize_prof.py)
+    traffic = load_traffic(f"r03_lyon8_pow2_{lp}x{ld}_n{n}.json") if ld in (8192, 16384) else None
     del prof, dm, out
     return {
         "value": n * ctx.world * steps / elapsed, "unit": "candidates/sec", "steps": steps,
@@ -628,7 +630,7 @@ def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2)
         "workload": f"{n} synthetic candidates per GPU: {lp}-bin profile + {ld}-byte DM array "
                     f"(a whole 128 x 128 PHCX DataBlock), 8 Lyon features (pfe_lyon8_u8)",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": (f"pfe::lyon8_u8_pow2<{lp}, {ld // 1024}>" if ld in (8192, 16384)
                                 else f"pfe::lyon8_u8_lds<{lp}, 112>" if ld == 15360
                                 else f"pfe::lyon8_u8_lds or lyon8_u8_long<{lp}>"),
