@@ -152,7 +152,11 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
   PFE_LA_CONTRACT
   static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
   const int gl = glane<G>();
-  double wa[N];
+  // nrm: the partial column norms MINPACK keeps in rdiag while it factors (literal build), or
+  // their squares (contracted build: the downdate r^2 - a^2, the pivot choice and the
+  // norm-loss test need no square root; only the columns' own norms ajnorm and acnorm do)
+  constexpr bool SQ = !LA_EXACT_QUOTIENTS;
+  double nrm[N], wa[N];
   {
     double s[N];
 #pragma unroll
@@ -166,20 +170,20 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       acnorm[j] = sqrt(s[j]);
-      rdiag[j] = acnorm[j];
-      wa[j] = acnorm[j];
+      nrm[j] = SQ ? s[j] : acnorm[j];
+      wa[j] = nrm[j];
       ipvt[j] = j;
     }
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     int kmax = j;
-    double rmax = rdiag[j];
+    double rmax = nrm[j];
 #pragma unroll
     for (int k = j + 1; k < N; ++k)
-      if (rdiag[k] > rmax) {
+      if (nrm[k] > rmax) {
         kmax = k;
-        rmax = rdiag[k];
+        rmax = nrm[k];
       }
     if (kmax != j) {
 #pragma unroll
@@ -191,7 +195,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
             a[s][j] = a[s][k2];
             a[s][k2] = t;
           }
-          rdiag[k2] = rdiag[j];
+          nrm[k2] = nrm[j];
           wa[k2] = wa[j];
           const int t = ipvt[j];
           ipvt[j] = ipvt[k2];
@@ -233,21 +237,25 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 #pragma unroll
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
-        if (rdiag[c] != 0.0) {
+        if (nrm[c] != 0.0) {
           const double ajc = gbcast<G>(a[0][c], j);
-          if (LA_EXACT_QUOTIENTS) {
-            const double t2 = ajc / rdiag[c];
-            rdiag[c] = rdiag[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
-          } else {  // rdiag sqrt(1 - (ajc/rdiag)^2) without the quotient
-            rdiag[c] = sqrt(fmax(0.0, (rdiag[c] - ajc) * (rdiag[c] + ajc)));
+          bool lost;
+          if constexpr (SQ) {  // r^2 - a^2, and 0.05 (r / wa)^2 <= epsmch on the squares
+            nrm[c] = fmax(0.0, nrm[c] - ajc * ajc);
+            lost = 0.05 * nrm[c] <= EPSMCH * wa[c];
+          } else {
+            const double t2 = ajc / nrm[c];
+            nrm[c] = nrm[c] * sqrt(fmax(0.0, 1.0 - t2 * t2));
+            lost = la_norm_lost(nrm[c], wa[c]);
           }
-          if (la_norm_lost(rdiag[c], wa[c])) {
+          if (lost) {
             double r = 0.0;
 #pragma unroll
             for (int k = 0; k < MPL; ++k)
               if (row_ge(gl, k, j + 1)) r += a[k][c] * a[k][c];
-            rdiag[c] = sqrt(gsum<G>(r));
-            wa[c] = rdiag[c];
+            r = gsum<G>(r);
+            nrm[c] = SQ ? r : sqrt(r);
+            wa[c] = nrm[c];
           }
         }
       }
