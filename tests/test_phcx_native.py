@@ -100,6 +100,14 @@ CASES = {
     "shape_mismatch": dict(nbins=3),                         # reshape error
     "partial_chunk": dict(block_text="\n" + "01" * 300 + "\n"),
     "no_dm_chunk": dict(block_text="\n0102\n"),
+    # runs of >= 16 hex digits (the reader's SSE2 path) with the quirks inside or at the edge
+    # of a 16-character chunk
+    "long_lower": dict(profile_text="\n" + "0a1b2c3d4e5f6a7b8c9d" * 4 + "\n"),
+    "long_bad_mid": dict(profile_text="\n" + "0A" * 10 + "G1" + "0B" * 10 + "\n"),
+    "long_odd_line": dict(profile_text="\n" + "0123456789ABCDEF0" + "\n" + "123456789ABCDEF" * 3 + "\n"),
+    "long_space_mid": dict(profile_text="\n" + "AB" * 12 + " C" + "DE" * 12 + "\n"),
+    "long_sign_mid": dict(profile_text="\n" + "AB" * 9 + "+C" + "DE" * 12 + "\n"),
+    "long_block_64": dict(block_text="\n" + "\n".join("%02X" * 32 % tuple((k * 7 + j) % 256 for j in range(32)) for k in range(64)) + "\n"),
 }
 
 
