@@ -207,11 +207,23 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
 #pragma unroll
     for (int k = 0; k < MPL; ++k)
       if (row_ge(gl, k, j)) p += a[k][j] * a[k][j];
-    double ajnorm = sqrt(gsum<G>(p));
+    // the column's norm and its reciprocal: sqrt and a division (literal build, or a sum of
+    // squares outside [1e-280, 1e280]), else one rsqrt and a product
+    const double pp = gsum<G>(p);
+    double ajnorm, rinv;
+    if (SQ && pp > 1e-280 && pp < 1e280) {
+      rinv = rsqrt(pp);
+      ajnorm = pp * rinv;
+    } else {
+      ajnorm = sqrt(pp);
+      rinv = 1.0 / ajnorm;
+    }
     rajjv[j] = 0.0;
     if (ajnorm != 0.0) {
-      if (gbcast<G>(a[0][j], j) < 0.0) ajnorm = -ajnorm;
-      const double rinv = 1.0 / ajnorm;
+      if (gbcast<G>(a[0][j], j) < 0.0) {
+        ajnorm = -ajnorm;
+        rinv = -rinv;
+      }
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) a[k][j] = la_quot(a[k][j], ajnorm, rinv);
