@@ -200,8 +200,11 @@ __device__ __forceinline__ void blm_init(const Fn& fcn, int f, BlmState<N, FPW>&
   blm_outer<N, MPL, FPW>(fcn, fvec, cache, fnorm, f, S, 1, 1);
 }
 
-// SIMT phase for this lane's fit: lmpar, the trial point and the predicted-reduction terms
-template <int N, int FPW>
+// SIMT phase for this lane's fit: lmpar, the trial point and the predicted-reduction terms.
+// ACN_SQ (the pooled engine's contracted build): S.acn holds the squared column norms of the
+// new Jacobian, and the scaling MINPACK updates after qrfac (diag = max(diag, acnorm); at
+// the first iteration diag = acnorm, xnorm and delta) is done here, one fit per lane
+template <int N, int FPW, bool ACN_SQ = false>
 __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
   PFE_LA_CONTRACT
   double r[N][N], diag[N], qtf[N], x[N];
@@ -222,7 +225,27 @@ __device__ __forceinline__ void blm_simt(int f, BlmState<N, FPW>& S) {
     // scaled gradient norm of the new Jacobian and the gtol test (lmdif's outer loop)
     double acn[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) acn[j] = S.acn[j][f];
+    for (int j = 0; j < N; ++j) acn[j] = ACN_SQ ? sqrt(S.acn[j][f]) : S.acn[j][f];
+    if constexpr (ACN_SQ) {
+      if (iter == 1) {
+        double wa3[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          diag[j] = acn[j] == 0.0 ? 1.0 : acn[j];
+          wa3[j] = diag[j] * x[j];
+        }
+        const double xnorm = enorm_u(wa3);
+        delta = LM_FACTOR * xnorm;
+        if (delta == 0.0) delta = LM_FACTOR;
+        S.xnorm[f] = xnorm;
+        S.delta[f] = delta;
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        diag[j] = fmax(diag[j], acn[j]);
+        S.diag[j][f] = diag[j];
+      }
+    }
     double gnorm = 0.0;
     if (fnorm != 0.0) {
       const double rfn = 1.0 / fnorm;

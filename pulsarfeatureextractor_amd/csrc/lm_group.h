@@ -169,8 +169,8 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
     gsum_from<N, G>(s, 0);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      acnorm[j] = sqrt(s[j]);
-      nrm[j] = SQ ? s[j] : acnorm[j];
+      acnorm[j] = SQ ? s[j] : sqrt(s[j]);  // squared in the contracted build (blm_simt roots it)
+      nrm[j] = acnorm[j];
       wa[j] = nrm[j];
       ipvt[j] = j;
     }
@@ -358,9 +358,13 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   int ipvt[N];
   double rdiag[N], acn[N], rajjv[N];
   qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn, rajjv);
+  // the contracted build leaves acn squared and the scaling (diag, and xnorm / delta of a
+  // fresh fit) to the next SIMT phase, one fit per lane (blm_simt<.., true>)
+  constexpr bool SQ = !LA_EXACT_QUOTIENTS;
   double diag[N];
   double xnorm = 0.0, delta = 0.0;
-  if (iter == 1) {
+  if (SQ) {
+  } else if (iter == 1) {
     double wa3[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -405,12 +409,12 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   if (gl == 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      S.diag[j][f] = fmax(diag[j], acn[j]);
+      if (!SQ) S.diag[j][f] = fmax(diag[j], acn[j]);
       S.qtf[j][f] = qtf[j];
       S.acn[j][f] = acn[j];
       S.ipvt[j][f] = ipvt[j];
     }
-    if (iter == 1) {
+    if (!SQ && iter == 1) {
       S.xnorm[f] = xnorm;
       S.delta[f] = delta;
     }
@@ -595,7 +599,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
 #endif
     // SIMT phase: the gtol test after a new Jacobian, lmpar, the trial point
     if (lane < FPW && ph[lane] == PH_LMPAR) {
-      blm_simt<N, FPW>(lane, S);
+      blm_simt<N, FPW, !LA_EXACT_QUOTIENTS>(lane, S);
       ph[lane] = S.info[lane] != 0 ? PH_DONE : PH_TRIAL;
     }
     blm_sync();
