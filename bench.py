@@ -481,7 +481,7 @@ def run_bates22(ctx, args, n, lp, steps, warmup, small_warm=False):
 
     elapsed, kern_ms, kern_max = ctx.time_steps(step, steps, warmup, warm)
     res = {
-        "metric": "candidates/sec (22-score path, 128-bin)",
+        "metric": f"candidates/sec (22-score path, {lp}-bin)",
         **common_fields(ctx, n, steps, warmup, elapsed),
         "dtype": "f64",
         "config": {
