@@ -755,7 +755,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
-constexpr int PFD4_E = 8;  // fold elements per thread and load step of k_pfd_dmprof4
+constexpr int PFD4_E = 16;  // fold elements per thread and load step of k_pfd_dmprof4
 
 // the accumulated sub-band rotations of the 100 trial DMs (PFDFile.py:395-416), one lane
 // per sub-band: rot[k][j] (the sweep of the single-wave kernel keeps them in cum / sdb)
