@@ -1,8 +1,8 @@
 #!/bin/bash
 # timing probe: the 22-score chain without qrfac's column swaps (libpfe_noswap.so, wrong
+# results, timing only) against the product library, serialised trace of each
 # (the PFE_PROBE_NO_PIVOT_SWAP hook in lm_group.h was removed after the probe; re-add
 # "kmax = j;" before the exchange and build variant noswap with that define to repeat it)
-# results, timing only) against the product library, serialised trace of each
 set -e
 set -o pipefail
 export TMPDIR=/tmp
