@@ -764,9 +764,10 @@ __global__ __launch_bounds__(256) void lyon8_f64_generic(const double* __restric
 namespace pfe {
 
 static inline int grid_for(int64_t work_waves, int cap) {
-  // 4 waves per block; capped (handle option PFE_OPT_LYON8_BLOCKS, default 256 CUs x 32
-  // blocks: 7 resident waves per SIMD at 71 VGPRs, +1-2 % over 8 blocks per CU,
-  // tools/ab_lyon8_grid.sh) and grid-stride the rest
+  // 4 waves per block; capped (handle option PFE_OPT_LYON8_BLOCKS, default 256 CUs x 64
+  // blocks: 7 resident waves per SIMD at 71 VGPRs; 32 blocks per CU were +1-2 % over 8
+  // (tools/ab_lyon8_grid.sh), 64 a further 1.3 % over 32 (profiles/r03_ab_lyon8_grid.txt))
+  // and grid-stride the rest
   int64_t blocks = (work_waves + 3) / 4;
   if (blocks < 1) blocks = 1;
   if (blocks > cap) blocks = cap;
