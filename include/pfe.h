@@ -114,6 +114,10 @@ int pfe_synchronize(pfe_handle* h);
  *   PFE_OPT_LYON8_BURST  candidate groups per wave step of the Lyon-8 kernel: 1, 2 or 4
  *                        (default 2)
  *   PFE_OPT_PFD_WAVES    waves per fold of the PFD preprocessing kernel: 4 (default) or 1
+ *   PFE_OPT_LYON8_DM     (bits) Lyon-8 kernel for DataBlock-length DM rows (PHCX nDM x 128
+ *                        bytes): 0 = per-byte LDS kernel with batched finalisation (default),
+ *                        1 = the round-3 kernels.  Mean and std are numpy's bits either way;
+ *                        skew / kurt may differ in the last bits (scipy's m2 vs the exact one)
  * Returns PFE_EINVAL for an unknown option or an out-of-range value.
  * --------------------------------------------------------------------------------------- */
 #define PFE_OPT_SOLVER 1
@@ -123,6 +127,7 @@ int pfe_synchronize(pfe_handle* h);
 #define PFE_OPT_LYON8_BLOCKS 5
 #define PFE_OPT_LYON8_BURST 6
 #define PFE_OPT_PFD_WAVES 7
+#define PFE_OPT_LYON8_DM 8
 #define PFE_SOLVER_POOLED 0
 #define PFE_SOLVER_BATCHED 1
 #define PFE_SOLVER_WAVE 2

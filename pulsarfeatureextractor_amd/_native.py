@@ -73,6 +73,7 @@ OPTIONS = {
     "lyon8_blocks": 5,
     "lyon8_burst": 6,
     "pfd_waves": 7,
+    "lyon8_dm": 8,      # 0 per-byte DataBlock kernel (default), 1 the round-3 kernels
 }
 SOLVERS = {"pooled": 0, "batched": 1, "wave": 2}
 

@@ -2,6 +2,7 @@
 
   python -m pulsarfeatureextractor_amd.cli -c <dir|file> -o <out> [--phcx|--superb]
          [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K] [--start K]
+         [--metrics FILE]
 
 Same flags, same output-file probing (:147-160), same mode dispatch (:215-290), for PHCX,
 SUPERB and PFD files in every mode, --label included (its prompt is commented out in the
@@ -32,7 +33,12 @@ def main(argv=None):
     p.add_option("--workers", action="store", dest="workers", type="int", default=None)
     # resume offset (not in the reference): skip the first K discovered candidates, e.g. the
     # ones a stopped collective run had already appended to its output file
+    # (collective modes also keep <output>.progress = the --start value that resumes after
+    # the last batch appended)
     p.add_option("--start", action="store", dest="start", type="int", default=0)
+    # structured per-run metrics (not in the reference): one JSON object written to FILE at
+    # the end of the run (candidates, successes, failures by reason, candidates/s, times)
+    p.add_option("--metrics", action="store", dest="metrics", type="string", default=None)
     args, _ = p.parse_args(argv)
     # output-file probing (:147-160)
     single_file = os.path.exists(args.outputPath)
@@ -53,7 +59,8 @@ def main(argv=None):
     from .candidate import get_engine
 
     get_engine(args.device)
-    dp = processor.DataProcessor(args.verbose, workers=args.workers, start=args.start)
+    dp = processor.DataProcessor(args.verbose, workers=args.workers, start=args.start,
+                                 metrics_path=args.metrics)
     phcx, pfd, superb = args.phcx, args.pfd, args.superb
     try:
         if args.label:  # :220-225 (labelPFD with the two arguments ScoreGenerator passes)

@@ -258,6 +258,10 @@ int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
       if (v != 1 && v != 4) break;
       o.pfd_waves = (int)v;
       return PFE_OK;
+    case PFE_OPT_LYON8_DM:
+      if (v != 0 && v != 1) break;
+      o.lyon8_dm = (int)v;
+      return PFE_OK;
     default:
       return set_err(h, PFE_EINVAL, "pfe_set_option: unknown option %d", option);
   }
@@ -276,6 +280,7 @@ int pfe_get_option(const pfe_handle* h, int32_t option, int64_t* v) {
     case PFE_OPT_LYON8_BLOCKS: *v = o.lyon8_blocks; return PFE_OK;
     case PFE_OPT_LYON8_BURST: *v = o.lyon8_burst; return PFE_OK;
     case PFE_OPT_PFD_WAVES: *v = o.pfd_waves; return PFE_OK;
+    case PFE_OPT_LYON8_DM: *v = o.lyon8_dm; return PFE_OK;
     default: return PFE_EINVAL;
   }
 }

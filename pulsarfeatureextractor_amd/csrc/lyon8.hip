@@ -716,6 +716,265 @@ __global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ 
   }
 }
 
+// ---- DataBlock rows, round 4: per-byte numpy chains at 4 VALU per byte ------------------
+// lyon8_u8_lds spends ~3.1 k VALU wave-instructions per 15 360-byte row (VALU-bound at 37 %
+// of HBM): byte extraction from 64-bit words, per-row 128-bit finalisation in every lane,
+// 64-bit wave reductions.  This kernel keeps numpy's arithmetic and removes the rest:
+//   * each byte of a leaf is read from the wave's padded LDS image with ds_read_u8 (the LDS
+//     unit zero-extends it: no VALU extraction), then cvt / sub / mul / add -- numpy's
+//     fl(fl(x - mean)^2) added to the leaf's running sum j = i mod 8 in order;
+//   * the exact power sums (mean, skew, kurt) come from the coalesced registers the row was
+//     loaded into, as the other Lyon-8 kernels compute them (v_dot4 / v_dot2);
+//   * the per-row totals are reduced as 32-bit halves (DPP in-row, permlane swaps across
+//     rows) and parked in lane (row mod 64); the 8 statistics of a batch of <= 64 rows are
+//     finalised once, one row per lane, and stored as one 4 KiB span -- the divisions,
+//     square roots and 128-bit numerators run once per 64 rows instead of once per row;
+//   * each wave owns a contiguous range of rows (no grid-stride tail imbalance).
+// Row layout (numpy): chunks of 8192 values (the first NCH-1 full: 64 leaves of 128), the
+// last chunk a perfect pairwise tree of `leaves` leaves of MW*8 values (host: dm_shape).
+// LDS image: leaf l at l*(m+4) (m+4 = 4 * odd, so the 32 lanes of a ds_read_u8 group hit 32
+// distinct banks), written with ds_write_b32 (the padded stride is only 4-byte aligned).
+struct DmShape {
+  int lp;          // profile length (64 / 128 / 256)
+  int ld;          // DataBlock row length (multiple of 16)
+  int np;          // 1 KiB load instructions per row = ceil(ld / 1024)
+  int len_last;    // bytes of the last chunk
+  int leaves_last; // leaves of the last chunk (power of two <= 64)
+  uint32_t magic;  // floor(o / m_last) = mulhi(o, magic) for o < 8208
+};
+
+constexpr int DM_S_FULL = 132;
+constexpr int DM_IMG_BYTES = 64 * DM_S_FULL;  // one chunk image per wave (8448 B)
+
+// 64-lane sum of a 32-bit value: DPP within rows, then the four row sums through the
+// permlane swaps.  Exact; every lane ends with the total.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)dpp_i32<DPP_QUAD_XOR1>((int)v);
+  v += (uint32_t)dpp_i32<DPP_QUAD_XOR2>((int)v);
+  v += (uint32_t)dpp_i32<DPP_ROW_HALF_MIRROR>((int)v);
+  v += (uint32_t)dpp_i32<DPP_ROW_MIRROR>((int)v);
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = a[0] + a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return b[0] + b[1];
+}
+
+// 8 numpy leaf chains over W words of the leaf at `lb` (LDS), each byte fl(fl(x-mean)^2).
+// The byte reads are volatile so that they stay single ds_read_u8 (zero-extended by the LDS
+// unit) instead of being merged into dword reads that need a VALU extraction per byte.
+template <int W>
+__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean) {
+  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
+  lds_u8* vb = (lds_u8*)lb;
+  // software pipeline: the 8 bytes of word k+1 are read while word k is computed
+  uint32_t cur[8], nxt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cur[j] = vb[j];
+  double r[8];
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    if (k + 1 < W) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) nxt[j] = vb[8 * (k + 1) + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double d = (double)cur[j] - mean;
+      const double sq = d * d;
+      r[j] = k == 0 ? sq : r[j] + sq;
+    }
+    // pin word k's arithmetic before word k+2's reads (empty asm ordered with the volatile
+    // reads; without it every read of the leaf is hoisted, one VGPR each)
+    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+  }
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+// write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image
+template <int NCH, int MW, int NPMAX>
+__device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], int ch, int lane,
+                                         uint32_t full_base, const DmShape& sh) {
+  constexpr int ML = 8 * MW;
+  constexpr bool SPLIT = (ML % 16) != 0;  // 16-B pieces straddle two leaves
+  typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;
+  if (ch < NCH - 1) {                     // full chunk: leaf lane/8 + 8j, stride 132
+    // (volatile: single ds_write_b32 with 16-bit immediate offsets from one base register,
+    // not ds_write2_b32 pairs whose 8-bit offsets need a base register per piece)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lds_u32* dst = (lds_u32*)(img + full_base + 1056 * j);
+      const u32x4 v = q[8 * ch + j];
+      dst[0] = v.x;
+      dst[1] = v.y;
+      dst[2] = v.z;
+      dst[3] = v.w;
+    }
+  } else {
+    // recomputed per row (a few VALU) rather than hoisted out of the row loop and spilled
+    uint32_t o0 = 16u * lane;
+    asm volatile("" : "+v"(o0));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t o = o0 + 1024u * j;  // chunk-relative byte offset
+      if (o < (uint32_t)sh.len_last) {  // (pieces of instructions >= np have o >= len_last)
+        const u32x4 v = q[8 * ch + j];
+        const uint32_t a0 = o + 4u * __umulhi(o, sh.magic);
+        if constexpr (SPLIT) {
+          const uint32_t a1 = o + 8u + 4u * __umulhi(o + 8u, sh.magic);
+          reinterpret_cast<uint32_t*>(img + a0)[0] = v.x;
+          reinterpret_cast<uint32_t*>(img + a0)[1] = v.y;
+          reinterpret_cast<uint32_t*>(img + a1)[0] = v.z;
+          reinterpret_cast<uint32_t*>(img + a1)[1] = v.w;
+        } else {
+          uint32_t* dst = reinterpret_cast<uint32_t*>(img + a0);
+          dst[0] = v.x;
+          dst[1] = v.y;
+          dst[2] = v.z;
+          dst[3] = v.w;
+        }
+      }
+    }
+  }
+}
+
+template <int NCH, int MW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps,
+                                                   const uint8_t* __restrict__ dm, int64_t ds,
+                                                   int64_t n, double* __restrict__ out,
+                                                   DmShape sh) {
+  static_assert(NCH >= 1 && NCH <= 2 && MW >= 9 && MW <= 16, "shape");
+  constexpr int NPMAX = 8 * NCH;
+  constexpr int ML = 8 * MW;            // leaf length of the last chunk
+  constexpr int SL = ML + 4;            // its LDS leaf stride
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
+  const int lane = threadIdx.x & 63;
+  uint8_t* img = lds[threadIdx.x >> 6];
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  // wave-uniform by construction; readfirstlane makes it provable (scalar row loop, SGPR
+  // buffer descriptors)
+  const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t r0 = n * wave / nwaves, r1 = n * (wave + 1) / nwaves;
+  const int ppl = sh.lp >> 4;                            // lanes holding the profile
+  const int pl = lane < ppl ? lane : 0;
+  int zpad = 0;  // zero bytes this lane reads past the row
+#pragma unroll
+  for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
+  const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
+  for (int64_t base = r0; base < r1; base += 64) {
+    const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
+    uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
+    uint32_t kP1 = 0, kP2 = 0, kP3 = 0, kP4l = 0, kP4h = 0;
+    double kssq = 0.0;
+    for (int i = 0; i < cnt; ++i) {
+      const int64_t c = base + i;
+      // ---- loads: piece p = lane + 64 k (16 B) through a buffer descriptor of the row's
+      // ld bytes, so pieces past the row read as zero bytes (corrected below)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint8_t*>(dm + c * ds), 0, sh.ld, 0x00020000);
+      const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
+      u32x4 q[NPMAX];
+#pragma unroll
+      for (int k = 0; k < NPMAX; ++k)
+        q[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * k, 2));
+      // ---- exact power sums of the DM row; a zero byte past the row adds y^3 = -2^21 and
+      // y^4 = 2^28 (y = x - 128) and nothing to sum x, sum x^2
+      Acc2 sd = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < NPMAX; ++k) acc2_x4(q[k], sd);
+      sd.t3 += zpad << 21;
+      sd.t4 -= (uint64_t)zpad << 28;
+      Acc2 sp = {0, 0, 0, 0};  // (every lane, no branch: a branch here drains vmcnt)
+      acc2_x4(pq, sp);
+      if (lane >= ppl) sp = (Acc2){0, 0, 0, 0};
+      // ---- numpy's sum of squared deviations, chunk by chunk through the LDS image
+      // (chunk 0 is staged before the mean is known, so its registers die early)
+      dm_stage<NCH, MW>(img, q, 0, lane, full_base, sh);
+      const uint32_t S1 = wave_sum_u32(sd.s1);
+      const double mean = (double)S1 / (double)sh.ld;
+      double ssq = 0.0;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (ch > 0) dm_stage<NCH, MW>(img, q, ch, lane, full_base, sh);
+        wave_lds_sync();
+        double leaf;
+        if (ch < NCH - 1) {
+          leaf = dm_leaf<16>(img + lane * DM_S_FULL, mean);
+        } else {
+          leaf = dm_leaf<MW>(img + lane * SL, mean);
+          leaf = lane < sh.leaves_last ? leaf : 0.0;
+        }
+        const double cs = wave_sum_f64(leaf);
+        ssq = ch == 0 ? cs : ssq + cs;
+        wave_lds_sync();
+      }
+      // ---- the other row totals, as exact 32-bit halves
+      const uint32_t S2 = wave_sum_u32(sd.s2);
+      const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
+      const uint32_t T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
+      const uint32_t T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
+      const uint32_t T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
+      const uint32_t P1 = (uint32_t)group_sum_i32<16>((int)sp.s1);
+      const uint32_t P2 = (uint32_t)group_sum_i32<16>((int)sp.s2);
+      const uint32_t P3 = (uint32_t)group_sum_i32<16>(sp.t3);
+      const uint32_t P4l = (uint32_t)group_sum_i32<16>((int)(sp.t4 & 0xFFFFFFu));
+      const uint32_t P4h = (uint32_t)group_sum_i32<16>((int)(sp.t4 >> 24));
+      // ---- park the row's totals in lane i (profile sums: lane 0's row-0 values)
+      const bool mine = lane == i;
+      kS1 = mine ? S1 : kS1;
+      kS2 = mine ? S2 : kS2;
+      kT3l = mine ? T3l : kT3l;
+      kT3h = mine ? T3h : kT3h;
+      kT4l = mine ? T4l : kT4l;
+      kT4h = mine ? T4h : kT4h;
+      kP1 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P1) : kP1;
+      kP2 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P2) : kP2;
+      kP3 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P3) : kP3;
+      kP4l = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4l) : kP4l;
+      kP4h = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4h) : kP4h;
+      kssq = mine ? ssq : kssq;
+    }
+    // ---- finalise the batch: lane i -> row base + i
+    if (lane < cnt) {
+      // profile (lp a power of two: every moment is the correctly rounded exact rational)
+      const long long L = sh.lp;
+      const long long S1p = (long long)kP1;
+      const long long T1p = S1p - 128ll * L;
+      const long long T2p = (long long)kP2 - 256ll * S1p + 16384ll * L;
+      const long long T3p = (long long)(int)kP3;
+      const uint64_t T4p = ((uint64_t)kP4h << 24) + (uint64_t)kP4l;
+      const Moments mp = moments_i64(L, T1p, T2p, T3p, T4p);
+      const double sdp = sqrt(mp.m2);
+      const bool zp = zero_var(mp);
+      // DM row: mean exact, std = numpy's sqrt(ssq / n), skew / kurt from the exact
+      // third / fourth moments over scipy's m2 = ssq / n
+      const long long D = sh.ld;
+      const long long S1 = (long long)kS1;
+      const long long T1 = S1 - 128ll * D;
+      const long long T2 = (long long)kS2 - 256ll * S1 + 16384ll * D;
+      const long long T3 = (long long)(int)kT3h * 65536ll + (long long)kT3l;
+      const uint64_t T4 = ((uint64_t)kT4h << 24) + (uint64_t)kT4l;
+      const Moments md = moments_i128(D, T1, T2, T3, T4);
+      const double dn = (double)D;
+      const double m2 = kssq / dn;
+      const double e = 2.220446049250313e-16 * md.mean;
+      const bool zd = m2 <= e * e;
+      const double sdd = sqrt(m2);
+      f64x2* o = reinterpret_cast<f64x2*>(out + (base + lane) * 8);
+      __builtin_nontemporal_store((f64x2){mp.mean, sdp}, o);
+      __builtin_nontemporal_store(
+          (f64x2){zp ? __builtin_nan("") : mp.m3 / (mp.m2 * sdp),
+                  zp ? __builtin_nan("") : mp.m4 / (mp.m2 * mp.m2) - 3.0}, o + 1);
+      __builtin_nontemporal_store((f64x2){md.mean, sdd}, o + 2);
+      __builtin_nontemporal_store(
+          (f64x2){zd ? __builtin_nan("") : md.m3 / (m2 * sdd),
+                  zd ? __builtin_nan("") : md.m4 / (m2 * m2) - 3.0}, o + 3);
+    }
+  }
+}
+
 // ---- fp64 rows (PFD) -------------------------------------------------------------------
 // Two-pass fp64, as numpy/scipy: mean = sum/n; m_k = mean((x-mean)^k) with d^3 = d^2*d and
 // d^4 = (d^2)^2 (scipy.stats._moment exponentiation by squares).  One wave per row.
@@ -809,12 +1068,86 @@ static bool long_row_shape(int ld, LongShape& sh) {
   return false;
 }
 
+// lyon8_u8_dm's layout of a DataBlock row: nch chunks of numpy's reduction, the last one a
+// perfect pairwise tree of <= 64 leaves of 8 * mw bytes (mw in 9..16)
+static bool dm_shape(int lp, int ld, DmShape& sh, int& nch, int& mw) {
+  if (ld <= 256 || ld > 16384 || ld % 16) return false;
+  nch = (ld + 8191) / 8192;
+  const int len = ld - 8192 * (nch - 1);
+  int m = 0, leaves = 0;
+  if (!perfect_chunk(len, m, leaves) || leaves > 64 || m % 8) return false;
+  sh.lp = lp;
+  sh.ld = ld;
+  sh.np = (ld + 1023) / 1024;
+  sh.len_last = len;
+  sh.leaves_last = leaves;
+  sh.magic = (uint32_t)((0x100000000ull + (uint64_t)m - 1) / (uint64_t)m);
+  mw = m / 8;
+  return true;
+}
+
+// blocks of K that fit on the device at once (occupancy x CUs), cached per kernel
+template <auto K>
+static int resident_blocks() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+  if (cached[dev] > 0) return cached[dev];
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K), 256, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1024;
+  }
+  cached[dev] = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+  return cached[dev];
+}
+
+template <int NCH, int MW>
+static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
+                             int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
+  constexpr auto K = lyon8_u8_dm<NCH, MW>;
+  int64_t blocks = resident_blocks<K>();
+  const int64_t need = (n + 3) / 4;  // at least one row per wave
+  if (blocks > need) blocks = need;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(K, dim3((unsigned)blocks), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
+}
+
+template <int NCH>
+static void launch_dm_mw(int mw, const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
+                         int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
+  switch (mw) {
+    case 9: launch_dm_kernel<NCH, 9>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 10: launch_dm_kernel<NCH, 10>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 11: launch_dm_kernel<NCH, 11>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 12: launch_dm_kernel<NCH, 12>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 13: launch_dm_kernel<NCH, 13>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 14: launch_dm_kernel<NCH, 14>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    case 15: launch_dm_kernel<NCH, 15>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+    default: launch_dm_kernel<NCH, 16>(prof, ps, dm, ds, n, out, sh, st, cap); break;
+  }
+}
+
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
                            int64_t ds, int ld, int64_t n, double* out, hipStream_t st,
                            const Options& o) {
   if (n <= 0) return hipSuccess;
   const bool aligned = ((uintptr_t)prof % 16 == 0) && ((uintptr_t)dm % 16 == 0) &&
                        (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  DmShape dsh{};
+  int dnch = 0, dmw = 0;
+  if (o.lyon8_dm == 0 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
+      ld != 16384 && dm_shape(lp, ld, dsh, dnch, dmw)) {
+    // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dm
+    if (dnch == 1)
+      launch_dm_mw<1>(dmw, prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks);
+    else
+      launch_dm_mw<2>(dmw, prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks);
+    return hipGetLastError();
+  }
   if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {
     const int U = o.lyon8_burst;  // 1, 2 (default) or 4 candidate groups per wave step
     const int cpw = 64 / (lp / 32) * U;

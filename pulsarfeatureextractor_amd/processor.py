@@ -23,7 +23,9 @@ from __future__ import annotations
 
 import datetime
 import fnmatch
+import json
 import os
+import time
 from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 
 import numpy as np
@@ -31,7 +33,7 @@ import numpy as np
 from . import pfd as _pfd
 from . import phcx as _phcx
 from . import writers
-from .candidate import get_engine, status_error
+from .candidate import GROUP_ERRORS, get_engine, status_error
 
 BATCH = 8192  # files per streamed batch
 
@@ -320,6 +322,69 @@ def default_workers() -> int:
     return max(1, n)
 
 
+def _write_progress(out_path, done):
+    """<out_path>.progress: the number of discovered candidates whose lines (or failures) are
+    in the outputs -- the --start value that resumes after the last completed batch."""
+    tmp = out_path + ".progress.tmp"
+    with open(tmp, "w") as f:
+        f.write(f"{done}\n")
+    os.replace(tmp, out_path + ".progress")
+
+
+class RunMetrics:
+    """Structured per-run metrics: candidates, successes, failures by
+    reason (the reference's messages; the score-group ones are the PFE_ST_* bits of
+    pfe_bates22), candidates/s, and the host time spent parsing (helper thread) and scoring
+    (GPU stage: pack, DMA, kernels).  The counts mirror DataProcessor.py:596-599."""
+
+    _BITS = {msg: name for (_bit, msg), name in zip(
+        GROUP_ERRORS, ("PFE_ST_SINE_FAIL", "PFE_ST_GAUSS_FAIL", "PFE_ST_DMFIT_FAIL",
+                       "PFE_ST_SUBBAND_FAIL", "PFE_ST_UNSUPPORTED"))}
+
+    def __init__(self, mode, start_offset=0):
+        self.mode = mode
+        self.start_offset = int(start_offset)
+        self.t0 = time.perf_counter()
+        self.parse_s = 0.0
+        self.score_s = 0.0
+        self.batches = 0
+        self.reasons = {}
+
+    def timed_parse(self, fn):
+        def wrapped(paths):
+            t = time.perf_counter()
+            try:
+                return fn(paths)
+            finally:
+                self.parse_s += time.perf_counter() - t
+        return wrapped
+
+    def timed_score(self, fn):
+        def wrapped(pre):
+            t = time.perf_counter()
+            try:
+                return fn(pre)
+            finally:
+                self.score_s += time.perf_counter() - t
+        return wrapped
+
+    def batch(self, res):
+        self.batches += 1
+        for e in res.err:
+            if e:
+                key = self._BITS.get(e) or str(e).strip().split("\n")[0][:120]
+                self.reasons[key] = self.reasons.get(key, 0) + 1
+
+    def finish(self, processed, ok, failed):
+        wall = time.perf_counter() - self.t0
+        return {"mode": self.mode, "start_offset": self.start_offset,
+                "candidates": int(processed), "successes": int(ok), "failures": int(failed),
+                "failures_by_reason": dict(sorted(self.reasons.items())),
+                "batches": self.batches, "wall_s": round(wall, 6),
+                "candidates_per_s": round(processed / wall, 3) if wall > 0 else None,
+                "parse_s": round(self.parse_s, 6), "score_s": round(self.score_s, 6)}
+
+
 class DataProcessor:
     """Same entry points and output semantics as DataProcessor.py, batched on the GPU.
 
@@ -329,8 +394,10 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18):
+                 start=0, gpu_batch=1 << 18, metrics_path=None):
         self.debug = debugFlag
+        self.metrics_path = metrics_path
+        self.metrics = None   # RunMetrics.as_dict() of the last mode run
         self.engine = engine
         self.workers = workers or default_workers()
         self.log = log
@@ -365,6 +432,11 @@ class DataProcessor:
             paths = paths[self.start:]
         return paths
 
+    def _resuming(self, out_path):
+        """A resumed run (start > 0) appends to the output the stopped run wrote: its ARFF
+        header is already there, so a second one would break the file."""
+        return self.start > 0 and os.path.exists(out_path)
+
     def _fail(self, cand, why):
         self.log(f"Error reading profile data :\n\t{why}\n{cand}  did not have scores generated.")
         writers.append_text(self.candidateErrorLog, cand + "\n")
@@ -381,10 +453,16 @@ class DataProcessor:
                                 "".join(batch_paths[i] + "\n" for i in failed))
         return failed
 
-    def _summary(self, processed, ok, failed, start, extra=""):
+    def _summary(self, processed, ok, failed, start, extra="", run=None):
         end = datetime.datetime.now()
         self.log(f"\nCandidates processed:\t{processed}\nSuccesses:\t{ok}\nFailures:\t{failed}\n"
                  f"{extra}Execution time:  {end - start}")
+        if run is not None:
+            self.metrics = run.finish(processed, ok, failed)
+            if self.metrics_path:
+                with open(self.metrics_path, "w") as f:
+                    json.dump(self.metrics, f, indent=1)
+                    f.write("\n")
 
     # ---- parse / score stages ---------------------------------------------------------
     def _parse(self, paths):
@@ -542,17 +620,20 @@ class DataProcessor:
             pre.close()
         return res
 
-    def _stream_text(self, paths, mode, out_path, style):
+    def _stream_text(self, paths, mode, out_path, style, run):
         """Collective modes: stream parse -> score, append each batch's lines (pfe_format_rows,
-        storeScore / storeScoreARFF text) in discovery order, log failures."""
+        storeScore / storeScoreARFF text) in discovery order, then log the batch's failures and
+        rewrite <out_path>.progress with the number of discovered candidates done (the --start
+        value that resumes after this batch)."""
         from ._native import format_rows
 
         counts = {"ok": 0, "failed": 0}
 
-        def emit(_off, batch_paths, res):
-            failed = self._fail_batch(batch_paths, res)
-            counts["failed"] += len(failed)
-            counts["ok"] += len(batch_paths) - len(failed)
+        def emit(off, batch_paths, res):
+            nfail = sum(1 for e in res.err if e)
+            counts["failed"] += nfail
+            counts["ok"] += len(batch_paths) - nfail
+            run.batch(res)
             mat, skip = _as_matrix(res)
             if mat is not None:
                 text = format_rows(batch_paths, mat, style, skip, threads=self.workers)
@@ -563,14 +644,17 @@ class DataProcessor:
             if text:
                 with open(out_path, "ab") as f:
                     f.write(text)
+            self._fail_batch(batch_paths, res)
+            _write_progress(out_path, self.start + off + len(batch_paths))
 
-        _stream(paths, self._parse, lambda pre: self._score(pre, mode), emit, self.batch)
+        _stream(paths, run.timed_parse(self._parse), run.timed_score(lambda pre: self._score(pre, mode)),
+                emit, self.batch)
         return counts["ok"], counts["failed"]
 
     # ---- 22 scores / profile bins ---------------------------------------------------
     def processCollectively(self, directory, verbose, regexes, outPath, arff, genProfileData,
                             single):
-        if arff:                                              # prepareARFFFile (:329-367)
+        if arff and not self._resuming(outPath):              # prepareARFFFile (:329-367)
             nattr = 22
             if genProfileData and self.superb:
                 nattr = 64
@@ -578,10 +662,11 @@ class DataProcessor:
                 nattr = 128
             writers.write_arff_header(outPath, writers.arff_header("scores", nattr))
         start = datetime.datetime.now()
-        paths = self._candidates(directory, regexes, single)
         mode = "profile" if genProfileData else "scores"
-        ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0)
-        self._summary(len(paths), ok, failed, start)
+        run = RunMetrics(mode, self.start)
+        paths = self._candidates(directory, regexes, single)
+        ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0, run)
+        self._summary(len(paths), ok, failed, start, run=run)
 
     def processPFDCollectively(self, directory, verbose, outPath, arff, genProfileData,
                                processSingleCandidate):
@@ -604,6 +689,7 @@ class DataProcessor:
     def processSeparately(self, directory, verbose, regexes, single):
         """:603-687 — each candidate's 22 scores into <candidate>.dat."""
         start = datetime.datetime.now()
+        run = RunMetrics("separately", self.start)
         paths = self._candidates(directory, regexes, single)
 
         from ._native import format_rows
@@ -614,6 +700,7 @@ class DataProcessor:
             failed = self._fail_batch(batch_paths, res)
             counts["failed"] += len(failed)
             counts["ok"] += len(batch_paths) - len(failed)
+            run.batch(res)
             mat, skip = _as_matrix(res)
             keep = [i for i in range(len(batch_paths)) if not res.err[i]]
             if mat is not None:
@@ -624,8 +711,9 @@ class DataProcessor:
                 with open(batch_paths[i] + ".dat", "w") as f:   # outputScores :429-447
                     f.write(t)
 
-        _stream(paths, self._parse, lambda pre: self._score(pre, "scores"), emit, self.batch)
-        self._summary(len(paths), counts["ok"], counts["failed"], start)
+        _stream(paths, run.timed_parse(self._parse),
+                run.timed_score(lambda pre: self._score(pre, "scores")), emit, self.batch)
+        self._summary(len(paths), counts["ok"], counts["failed"], start, run=run)
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
         self.phcx = True
@@ -633,12 +721,13 @@ class DataProcessor:
 
     # ---- 8 Lyon features -------------------------------------------------------------
     def dmprof(self, directory, verbose, regexes, outPath, arff, single):
-        if arff:
+        if arff and not self._resuming(outPath):
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
+        run = RunMetrics("lyon8", self.start)
         paths = self._candidates(directory, regexes, single)
-        ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0)
-        self._summary(len(paths), ok, failed, start)
+        ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0, run)
+        self._summary(len(paths), ok, failed, start, run=run)
 
     def dmprofPFD(self, directory, verbose, outPath, arff, processSingleCandidate):
         self.pfd = True
@@ -681,7 +770,8 @@ class DataProcessor:
         files = {"scores": directory + "/Scores.csv", "profile": directory + "/Profile.csv",
                  "dm": directory + "/DMCurve.csv"}
         start = datetime.datetime.now()
-        paths = discover(directory, regexes)
+        run = RunMetrics("label", self.start)
+        paths = self._candidates(directory, regexes, False)
         lab = "0"
         out = {k: [] for k in ("scores", "profile", "dm", "meta")}
 
@@ -695,7 +785,8 @@ class DataProcessor:
         counts = {"ok": 0, "failed": 0}
 
         def emit(_off, batch_paths, res):
-            failed = self._fail_batch(batch_paths, res)
+            run.batch(res)
+            failed = [i for i, e in enumerate(res.err) if e]
             counts["failed"] += len(failed)
             for i, p in enumerate(batch_paths):
                 if not res.err[i]:
@@ -706,10 +797,12 @@ class DataProcessor:
                 if out[k]:
                     writers.append_text(path, "".join(out[k]))
                     out[k].clear()
+            self._fail_batch(batch_paths, res)
 
-        _stream(paths, self._parse, lambda pre: self._score(pre, "label"), emit, self.batch)
+        _stream(paths, run.timed_parse(self._parse),
+                run.timed_score(lambda pre: self._score(pre, "label")), emit, self.batch)
         self._summary(len(paths), counts["ok"], counts["failed"], start,
-                      f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n")
+                      f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n", run=run)
 
     def labelPHCX(self, directory, verbose):
         self.phcx = True

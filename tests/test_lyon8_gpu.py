@@ -109,6 +109,33 @@ def test_long_dm_rows_vs_oracle(engine, lp, ld):
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
+@pytest.mark.parametrize("ld", [15360, 12800, 9216])
+def test_long_dm_rows_multibatch(engine, ld):
+    """lyon8_u8_dm with one block (4 waves) over 600 rows: every wave runs several batches of
+    up to 64 rows (finalised one row per lane), the last one partial.  Bit-identical to the
+    default grid, mean/std bit-exact against the oracle."""
+    prof, dm = lyon_batch(600, 128, ld, seed=3 + ld, adversarial=True)
+    ref = engine.lyon8(prof, dm)
+    with engine.options(lyon8_blocks=1):
+        got = engine.lyon8(prof, dm)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
+
+
+def test_long_dm_rows_kernel_options_agree(engine):
+    """The round-3 DataBlock kernels (PFE_OPT_LYON8_DM = 1) and lyon8_u8_dm give the same
+    mean/std bits; skew/kurt agree to 1e-12 (scipy's m2 vs the exact one)."""
+    prof, dm = lyon_batch(400, 128, 15360, seed=77, adversarial=True)
+    a = engine.lyon8(prof, dm)
+    with engine.options(lyon8_dm=1):
+        b = engine.lyon8(prof, dm)
+    for c in (0, 1, 4, 5):
+        assert np.array_equal(a[:, c], b[:, c], equal_nan=True)
+    m = ~np.isnan(b)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    assert (np.abs(a - b)[m] / np.maximum(1, np.abs(b[m]))).max() <= TOL
+
+
 @pytest.mark.parametrize("ld", [16256, 4352, 30720])
 def test_long_dm_rows_other_lengths(engine, ld):
     """DataBlock lengths whose numpy pairwise trees are not perfect (nDM = 127, 34, 240):

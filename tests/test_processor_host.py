@@ -146,6 +146,63 @@ def test_resume_offset(tmp_path, monkeypatch):
     assert open(part).read().splitlines() == want
 
 
+def test_resume_offset_arff_single_header(tmp_path, monkeypatch):
+    """Resuming an --arff run appends rows to the stopped run's file without a second
+    '@relation ... @data' header; the .progress marker holds the --start value to resume."""
+    monkeypatch.chdir(tmp_path)
+    d = make_dir(tmp_path)
+    full = str(tmp_path / "full.arff")
+    part = str(tmp_path / "part.arff")
+    paths = processor.discover(d + "/", [processor.PHCX_RE])
+
+    def run(path, start):
+        dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=lambda *a: None,
+                                     batch=8, start=start)
+        dp._slabs = PlainSlabs()
+        dp.processPHCXCollectively(d + "/", False, path, True, False, False)
+
+    run(full, 0)
+    assert int(open(full + ".progress").read()) == len(paths)
+    # a "stopped" run: the header and the lines of the first 16 candidates
+    text = open(full).read()
+    head, body = text.split("@data\n")
+    done = set(paths[:16])
+    first = [ln for ln in body.splitlines() if ln.split(",?%")[-1] in done]
+    with open(part, "w") as f:
+        f.write(head + "@data\n" + "".join(ln + "\n" for ln in first))
+    run(part, 16)
+    got = open(part).read()
+    assert got.count("@relation") == 1 and got.count("@data") == 1
+    assert got == text
+    assert int(open(part + ".progress").read()) == len(paths)
+
+
+def test_run_metrics_json(tmp_path, monkeypatch):
+    """--metrics: one JSON object per run with the reference's counts (DataProcessor.py:596-599)
+    and failures by reason (PFE_ST_* names for the score groups)."""
+    import json
+
+    monkeypatch.chdir(tmp_path)
+    d = make_dir(tmp_path)
+    out = str(tmp_path / "s.csv")
+    mpath = str(tmp_path / "m.json")
+    dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=lambda *a: None, batch=8,
+                                 metrics_path=mpath)
+    dp._slabs = PlainSlabs()
+    dp.processPHCXCollectively(d + "/", False, out, False, False, False)
+    m = json.load(open(mpath))
+    assert m == dp.metrics
+    paths = processor.discover(d + "/", [processor.PHCX_RE])
+    ok_lines, failed = expected(paths, "scores")
+    assert m["mode"] == "scores" and m["candidates"] == len(paths)
+    assert m["successes"] == len(ok_lines) and m["failures"] == len(failed)
+    assert sum(m["failures_by_reason"].values()) == len(failed)
+    assert m["failures_by_reason"].get("PFE_ST_GAUSS_FAIL", 0) >= 1
+    assert m["batches"] == -(-len(paths) // 8)
+    for k in ("wall_s", "candidates_per_s", "parse_s", "score_s"):
+        assert m[k] is not None and m[k] >= 0
+
+
 def test_stream_dmprof_lyon8(tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     d = make_dir(tmp_path)

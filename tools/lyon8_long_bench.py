@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--lp", type=int, default=128)
     ap.add_argument("--ld", default="16384,15360")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="handle option name=value (e.g. lyon8_dm=1), repeatable")
     args = ap.parse_args()
     import torch
 
@@ -30,6 +32,9 @@ def main():
     st = torch.cuda.Stream()
     torch.cuda.set_stream(st)
     eng.set_stream(st.cuda_stream)
+    opts = {k: int(v) for k, v in (o.split("=") for o in args.opt)}
+    for k, v in opts.items():
+        eng.set_option(k, v)
     for ld in (int(v) for v in args.ld.split(",")):
         prof, dm = lyon_batch_torch(args.n, args.lp, ld, seed=20261023, device="cuda")
         out = torch.empty((args.n, 8), dtype=torch.float64, device="cuda")
@@ -45,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         nb = (args.lp + ld + 64) * args.n
-        print(json.dumps({"lp": args.lp, "ld": ld, "n": args.n, "avg_kernel_ms": ms,
+        print(json.dumps({"lp": args.lp, "ld": ld, "n": args.n, "opts": opts, "avg_kernel_ms": ms,
                           "candidates_per_s": args.n / ms * 1e3,
                           "algorithmic_GBps": nb / ms / 1e6, "frac_of_8TBps": nb / ms / 8e9}),
               flush=True)
