@@ -59,6 +59,24 @@ def status_error(st: int) -> str | None:
     return None
 
 
+def band_sum(rows):
+    """PHCXOperations.getSubbandData / getSubintData post-processing (:440-464), with the
+    reference's statements kept: ``sum_ = [0] * 128`` then ``sum_ += row - mean(row)`` per
+    row.  Python tries the number protocol before list concatenation, so the first ``+=``
+    turns the list into ndarray.__radd__'s float64 array and the rows are summed element by
+    element in order (a row of another length raises, as in the reference); then negatives
+    become 0.0.  Pinned by tests/golden/getters_phcx128.npz.  Host data getter (no score is
+    computed from it; the reference's callers are commented out, DataProcessor.py:749-750)."""
+    out = [0] * 128
+    for r in np.asarray(rows):
+        r = np.asarray(r)
+        out += r - np.mean(r)
+    for i in range(len(out)):
+        if out[i] < 0:
+            out[i] = 0.0
+    return out
+
+
 class CandidateFileInterface:
     """CandidateFileInterface.py:38-194 — per-format scorer interface."""
 
@@ -169,6 +187,14 @@ class PHCXFile(CandidateFileInterface):
     def getDMCurveData(self):
         """:306-318 — the decoded section-0 DataBlock."""
         return np.asarray(self.data.lyon_dm)
+
+    def getSubbandData(self):
+        """:704-716 -> PHCXOperations.getSubbandData (:422-464)."""
+        return band_sum(_phcx.band_rows(self.cand, "SubBands", self.SUPERB))
+
+    def getSubintData(self):
+        """:688-700 -> PHCXOperations.getSubintData (:468-505)."""
+        return band_sum(_phcx.band_rows(self.cand, "SubIntegrations", self.SUPERB))
 
 
 class SUPERBPHCXFile(PHCXFile):
@@ -291,6 +317,20 @@ class Candidate:
         if ".pfd" not in self.candidateName and ".gz" not in self.candidateName:
             return []
         self.scores = self._file(verbose).getDMCurveData()
+        return self.scores
+
+    def getSubbandData(self, verbose):
+        """Candidate.py:290-313: gzipped PHCX files only; [] for PFD and SUPERB PHCX."""
+        if ".pfd" in self.candidateName or ".gz" not in self.candidateName:
+            return []
+        self.scores = self._file(verbose).getSubbandData()
+        return self.scores
+
+    def getSubintData(self, verbose):
+        """Candidate.py:317-340: gzipped PHCX files only; [] for PFD and SUPERB PHCX."""
+        if ".pfd" in self.candidateName or ".gz" not in self.candidateName:
+            return []
+        self.scores = self._file(verbose).getSubintData()
         return self.scores
 
     def getScore(self, index):

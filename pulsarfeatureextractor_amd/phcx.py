@@ -100,6 +100,17 @@ def _read_xml(path: str, superb: bool):
     return ET.fromstring(data)
 
 
+def band_rows(path: str, tag: str, superb: bool | None = None) -> np.ndarray:
+    """PHCXOperations.getSubbandData / getSubintData (:434-438, :479-483): the hex block of
+    ``getElementsByTagName(tag)[1]`` (always element 1) as an (nSub, nBins) integer array
+    (hexToDec :353-383).  IndexError when the file has fewer than two such elements."""
+    if superb is None:
+        superb = ".gz" not in path
+    root = _read_xml(path, superb)
+    el = list(root.iter(tag))[1]
+    return hex_decode(el.text).reshape(int(el.get("nSub")), int(el.get("nBins")))
+
+
 def parse(path: str, superb: bool | None = None) -> PHCXCandidate:
     """Parse a PHCX (gzip) or SUPERB PHCX file the way Candidate.py:141-150 dispatches:
     names containing '.gz' are HTRU PHCX (section 1), anything else SUPERB (section 0)."""
@@ -155,10 +166,11 @@ def make_datablock(curve: np.ndarray, rng: np.random.Generator) -> np.ndarray:
 
 
 def write(path: str, *, profile, subbands, datablocks, dm_start, dm_end, n_dm_index,
-          period_s, snr, dm, width, superb: bool = False):
+          period_s, snr, dm, width, superb: bool = False, subints=None):
     """Write a synthetic candidate with two <Section>s.
 
-    Both sections carry the same profile, sub-bands, DmIndex and best values;
+    Both sections carry the same profile, sub-bands, DmIndex and best values (and, when
+    ``subints`` (nsubint x nbins) is given, the same <SubIntegrations> block);
     ``datablocks = (block0, block1)`` are the two sections' DataBlocks.  The Lyon DM array
     is always block0 (PHCXOperations.py:538); the DM-curve fit reads the scored section's
     block (1 for PHCX, 0 for SUPERB).  Returns the scored section index."""
@@ -176,6 +188,10 @@ def write(path: str, *, profile, subbands, datablocks, dm_start, dm_end, n_dm_in
                      f"<Snr>{snr!r}</Snr>\n<Width>{width!r}</Width>\n</BestValues>\n")
         parts.append(f"<SubBands nBins='{nb}' nSub='{nsub}' format='02X'>"
                      f"{_hex_lines(sbs.reshape(-1))}</SubBands>\n")
+        if subints is not None:
+            si = np.asarray(subints)
+            parts.append(f"<SubIntegrations nBins='{si.shape[1]}' nSub='{si.shape[0]}' "
+                         f"format='02X'>{_hex_lines(si.reshape(-1))}</SubIntegrations>\n")
         parts.append(f"<Profile nBins='{len(prof)}' format='02X'>{_hex_lines(prof)}</Profile>\n")
         parts.append(f"<DmCurve><DmIndex>{dmtext}</DmIndex></DmCurve>\n")
         parts.append(f"<DataBlock format='02X'>{_hex_lines(blk)}</DataBlock>\n")

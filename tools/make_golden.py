@@ -103,6 +103,10 @@ for f in files:
             v = [float(x) for x in a + b]
         elif mode == "profile":
             v = [float(x) for x in c.calculateProfileScores(False)]
+        elif mode == "getters":
+            v = {"subband": [float(x) for x in c.getSubbandData(False)],
+                 "subint": [float(x) for x in c.getSubintData(False)],
+                 "subband_types": sorted({type(x).__name__ for x in c.getSubbandData(False)})}
         elif mode == "all30":
             a = list(c.calculateProfileStatScores(False))
             b = list(c.calculateDMCurveStatScores(False))
@@ -438,6 +442,49 @@ def make_label_golden(manifest):
                                      "pfd_shape": [8, 16, 64]}
 
 
+def make_getters_golden(manifest):
+    """Candidate.getSubbandData / getSubintData (Candidate.py:290-340 ->
+    PHCXOperations.py:422-505) on PHCX files that carry <SubIntegrations>; rows 0-1
+    adversarial (constant / all-zero sub-integrations)."""
+    from pulsarfeatureextractor_amd.synth import _rows_numpy
+
+    n, seed = 12, 20262015
+    rng = np.random.default_rng(seed)
+    prof, sub, curve, blocks, period, dmv, snr, width = bates_set(rng, n, 128, 16, 128, 128, False)
+    subints = _rows_numpy(rng, n * 32, 128, 20.0, 150.0).reshape(n, 32, 128)
+    subints[0] = 77
+    subints[1] = 0
+    arrays = dict(n=n, prof=prof, sub=sub, block0=_rows_lyon(rng, n, 128), block1=blocks,
+                  period=period, dm=dmv, snr=snr, width=width, dm_start=0.0, dm_end=200.0,
+                  n_dm_index=101)
+    from pulsarfeatureextractor_amd import phcx
+
+    with tempfile.TemporaryDirectory(prefix="pfe_golden_getters_") as tmp:
+        refdir = build_reference(tmp)
+        d = os.path.join(tmp, "getters")
+        os.makedirs(d)
+        files = []
+        for i in range(n):
+            p = os.path.join(d, f"getters_{i:05d}.phcx.gz")
+            phcx.write(p, profile=prof[i], subbands=sub[i], datablocks=(arrays["block0"][i], blocks[i]),
+                       dm_start=0.0, dm_end=200.0, n_dm_index=101, period_s=float(period[i]),
+                       snr=float(snr[i]), dm=float(dmv[i]), width=float(width[i]),
+                       subints=subints[i])
+            files.append(p)
+        res = run_reference(refdir, files, "getters", tmp)
+    assert all(r["ok"] for r in res), res
+    np.savez_compressed(
+        os.path.join(GOLDEN, "getters_phcx128.npz"), prof=prof.astype(np.uint8),
+        sub=sub.astype(np.uint8), subints=subints.astype(np.uint8),
+        block0=np.asarray(arrays["block0"]).astype(np.uint8), block1=blocks.astype(np.uint8),
+        period=period, dm=dmv, snr=snr, width=width,
+        subband=np.array([r["v"]["subband"] for r in res]),
+        subint=np.array([r["v"]["subint"] for r in res]),
+        subband_types=np.array([",".join(r["v"]["subband_types"]) for r in res]))
+    manifest["sets"]["getters_phcx128"] = {"mode": "Candidate.getSubbandData/getSubintData",
+                                           "seed": seed, "n": n, "subints": [32, 128]}
+
+
 def _rows_lyon(rng, n, L):
     from pulsarfeatureextractor_amd.synth import _rows_numpy
 
@@ -449,6 +496,12 @@ if __name__ == "__main__":
         mpath = os.path.join(GOLDEN, "manifest.json")
         man = json.load(open(mpath))
         make_pfd_golden(man)
+        with open(mpath, "w") as f:
+            json.dump(man, f, indent=1)
+    elif "--getters" in sys.argv:  # the Candidate getters golden only
+        mpath = os.path.join(GOLDEN, "manifest.json")
+        man = json.load(open(mpath))
+        make_getters_golden(man)
         with open(mpath, "w") as f:
             json.dump(man, f, indent=1)
     elif "--label" in sys.argv:  # the --label golden only
