@@ -20,13 +20,15 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return (n * rank) // world, (n * (rank + 1)) // world
 
 
-def init_from_env(backend: str | None = None):
-    """Initialise the default process group from RANK/WORLD_SIZE/MASTER_* (127.0.0.1)."""
+def init_from_env(backend: str | None = None, group_at_one: bool = False):
+    """Initialise the default process group from RANK/WORLD_SIZE/MASTER_* (127.0.0.1).
+    With WORLD_SIZE = 1 no group is made unless `group_at_one` (a one-rank RCCL group, so
+    the collective path can run on a single GPU)."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world == 1:
+    if world == 1 and not group_at_one:
         return 0, 1
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
@@ -72,6 +74,6 @@ def score_sharded(score_fn, arrays: dict, n_total: int, gather: bool = True, gro
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     lo, hi = shard_bounds(n_total, world, rank)
     local = score_fn(**{k: v[lo:hi] for k, v in arrays.items()})
-    if world == 1 or not gather:
+    if not gather or not dist.is_initialized():
         return local
     return gather_rows(local, n_total, group)

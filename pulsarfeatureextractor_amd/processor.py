@@ -230,19 +230,47 @@ def score_lyon8(cands, engine=None):
     return out
 
 
-def _stream(paths, parse, score, emit, batch=BATCH):
-    """parse(batch paths) on a helper thread one batch ahead of score(parsed) on the calling
-    thread; emit(batch offset, batch paths, results) in discovery order."""
+def _stream(paths, parse, score, emit, batch=BATCH, depth=1):
+    """parse(batch paths) on a helper thread, ahead of the GPU stage; score(parsed, slot) of
+    batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
+    once, each on its own engine handle and pinned slabs); emit(batch offset, batch paths,
+    results) on the calling thread in discovery order, overlapping the next batches'
+    scoring."""
     if not paths:
         return
     cuts = list(range(0, len(paths), batch)) + [len(paths)]
-    with ThreadPoolExecutor(max_workers=1) as ex:
-        fut = ex.submit(parse, paths[cuts[0]:cuts[1]])
-        for k in range(len(cuts) - 1):
-            parsed = fut.result()
-            if k + 2 < len(cuts):
-                fut = ex.submit(parse, paths[cuts[k + 1]:cuts[k + 2]])
-            emit(cuts[k], paths[cuts[k]:cuts[k + 1]], score(parsed))
+    nb = len(cuts) - 1
+
+    def part(k):
+        return paths[cuts[k]:cuts[k + 1]]
+
+    slots = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]
+    try:
+        with ThreadPoolExecutor(max_workers=1) as px:
+            parsed, scored = {}, {}
+
+            def submit_parse(k):
+                if k < nb and k not in parsed and k not in scored:
+                    parsed[k] = px.submit(parse, part(k))
+
+            def submit_score(k):
+                if k < nb and k not in scored:
+                    submit_parse(k)
+                    f = parsed.pop(k)
+                    scored[k] = slots[k % depth].submit(lambda f=f, k=k: score(f.result(), k % depth))
+
+            for k in range(min(depth + 1, nb)):
+                submit_parse(k)
+            for k in range(min(depth, nb)):
+                submit_score(k)
+            for k in range(nb):
+                res = scored.pop(k).result()
+                submit_score(k + depth)
+                submit_parse(k + depth + 1)
+                emit(cuts[k], part(k), res)
+    finally:
+        for ex in slots:
+            ex.shutdown(wait=True)
 
 
 class PinnedSlabs:
@@ -360,10 +388,10 @@ class RunMetrics:
         return wrapped
 
     def timed_score(self, fn):
-        def wrapped(pre):
+        def wrapped(pre, slot=0):
             t = time.perf_counter()
             try:
-                return fn(pre)
+                return fn(pre, slot)
             finally:
                 self.score_s += time.perf_counter() - t
         return wrapped
@@ -394,7 +422,7 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18, metrics_path=None):
+                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2):
         self.debug = debugFlag
         self.metrics_path = metrics_path
         self.metrics = None   # RunMetrics.as_dict() of the last mode run
@@ -411,7 +439,11 @@ class DataProcessor:
         self.pfd = False
         self.positive = 0
         self.negative = 0
-        self._slabs = PinnedSlabs()
+        # gpu_depth batches are scored at once (processor._stream), each slot with its own
+        # engine handle (stream + workspace) and pinned slabs
+        self.depth = max(1, int(gpu_depth))
+        self._slabs = [PinnedSlabs() for _ in range(self.depth)]
+        self._engines = {}
         if not os.path.exists(self.candidateErrorLog):       # :86-87
             writers.append_text(self.candidateErrorLog, "")
 
@@ -484,15 +516,30 @@ class DataProcessor:
         pre.rd = [_read_pfd(paths[i]) for i in pre.pf]
         return pre
 
-    def _eng(self):
-        return self.engine or get_engine()
+    def _eng(self, slot=0):
+        """Slot 0: the caller's engine (or the process default); slot k > 0: a second libpfe
+        handle on the same device (a handle's stream and workspace serve one call at a
+        time).  A non-libpfe engine (a test stub) serves every slot."""
+        from ._native import Engine
 
-    def _bates_native(self, pre, mat, err):
+        base = self.engine or get_engine()
+        if slot == 0 or not isinstance(base, Engine):
+            return base
+        e = self._engines.get(slot)
+        if e is None:
+            e = self._engines[slot] = Engine(base.device)
+        return e
+
+    def _slab(self, slot):
+        s = self._slabs
+        return s[slot % len(s)] if isinstance(s, list) else s
+
+    def _bates_native(self, pre, mat, err, slot=0):
         """22 scores of the reader's good files: one pfe_phcx_pack per (shape, chunk) into
         pinned slabs, pfe_bates22 on them (DataProcessor.py:491-525 batched)."""
         from ._native import PfeError
 
-        info, px, sl = pre.info, pre.px, self._slabs
+        info, px, sl = pre.info, pre.px, self._slab(slot)
         ok = np.flatnonzero(info["status"] == 0)
         keys = np.stack([info["lp"], info["nsub"], info["lsb"], info["ndm"]], 1)[ok]
         for (lp, nsub, lsb, ndm), rows in _groups(keys, ok):
@@ -508,7 +555,7 @@ class DataProcessor:
                 o = sl.view("out22", (m, 22), np.float64)
                 st = sl.view("status", (m,), np.uint32)
                 try:
-                    self._eng().bates22(a["prof"], a["sub"], a["dmcurve"], a["scal"], out=o,
+                    self._eng(slot).bates22(a["prof"], a["sub"], a["dmcurve"], a["scal"], out=o,
                                         status=st)
                 except PfeError as e:  # a shape the library refuses fails its rows, not the run
                     for d in dst:
@@ -530,15 +577,16 @@ class DataProcessor:
                 cands.append(c)
         return idx, cands
 
-    def _score_phcx(self, pre, mode, res):
-        info, px, sl = pre.info, pre.px, self._slabs
+    def _score_phcx(self, pre, mode, res, slot=0):
+        info, px, sl = pre.info, pre.px, self._slab(slot)
+        eng = self._eng(slot)
         ok = np.flatnonzero(info["status"] == 0)
         fidx, fcands = self._fallback_cands(pre, res)
         if mode in ("scores", "label"):
             mat = res.mat if mode == "scores" else np.full((len(pre.paths), 22), np.nan)
-            self._bates_native(pre, mat, res.err)
+            self._bates_native(pre, mat, res.err, slot)
             if fcands:
-                sc, errs = score_bates(fcands, self.engine)
+                sc, errs = score_bates(fcands, eng)
                 for j, i in enumerate(fidx):
                     mat[i], res.err[i] = sc[j], errs[j]
             if mode == "label":  # Candidate.calculateProfileScores / getDMCurveData
@@ -564,10 +612,10 @@ class DataProcessor:
                     r = rows[s0:s0 + self.gpu_batch]
                     a = pre.nb.pack(r, lp=lp, ld=ld, alloc=sl.view, threads=self.workers)
                     o = sl.view("out8", (len(r), 8), np.float64)
-                    self._eng().lyon8(a["prof"], a["lyon_dm"], out=o)
+                    eng.lyon8(a["prof"], a["lyon_dm"], out=o)
                     res.mat[px[r]] = o
             if fcands:
-                f = score_lyon8(fcands, self.engine)
+                f = score_lyon8(fcands, eng)
                 res.mat[fidx] = f
         else:  # "profile": the profile bins as float scores (PHCXFile.computeProfileScores)
             keys = info["lp"][ok][:, None]
@@ -578,8 +626,9 @@ class DataProcessor:
             for j, i in enumerate(fidx):
                 res.rows[i] = np.asarray(fcands[j].profile, dtype=np.float64)
 
-    def _score_pfd(self, pre, mode, res):
+    def _score_pfd(self, pre, mode, res, slot=0):
         pf, rd = pre.pf, pre.rd
+        eng = self._eng(slot)
         good = [k for k, (d, e) in enumerate(rd) if d is not None]
         for k, (d, e) in enumerate(rd):
             if d is None:
@@ -588,17 +637,17 @@ class DataProcessor:
         if not datas:
             return
         if mode == "profile":       # PFDFile.computeProfileScores (:479-492)
-            _f, profiles, _e = score_pfd(datas, self.engine)
+            _f, profiles, _e = score_pfd(datas, eng)
             for j, k in enumerate(good):
                 res.rows[pf[k]] = np.asarray(profiles[j], dtype=np.float64)
         elif mode == "lyon8":
-            feats, _prof, errs = score_pfd(datas, self.engine)
+            feats, _prof, errs = score_pfd(datas, eng)
             for j, k in enumerate(good):
                 res.mat[pf[k]], res.err[pf[k]] = feats[j], errs[j]
         else:
-            sc, errs = score_pfd22(datas, self.engine)
+            sc, errs = score_pfd22(datas, eng)
             if mode == "label":
-                prof, chis, derr = pfd_profile_and_curve(datas, self.engine)
+                prof, chis, derr = pfd_profile_and_curve(datas, eng)
                 for j, k in enumerate(good):
                     res.err[pf[k]] = errs[j] or derr[j]
                     res.rows[pf[k]] = (sc[j], [float(v) for v in prof[j]], list(chis[j]))
@@ -606,16 +655,17 @@ class DataProcessor:
                 for j, k in enumerate(good):
                     res.mat[pf[k]], res.err[pf[k]] = sc[j], errs[j]
 
-    def _score(self, pre, mode):
-        """GPU stage.  mode: "scores" (22 scores), "profile" (profile bins), "lyon8" (the 8
-        Lyon features) or "label" ((scores, profile, DM-curve data)) -> BatchScores."""
+    def _score(self, pre, mode, slot=0):
+        """GPU stage on pipeline slot `slot`.  mode: "scores" (22 scores), "profile" (profile
+        bins), "lyon8" (the 8 Lyon features) or "label" ((scores, profile, DM-curve data))
+        -> BatchScores."""
         width = {"scores": 22, "lyon8": 8}.get(mode)
         res = BatchScores(len(pre.paths), width)
         try:
             if len(pre.px):
-                self._score_phcx(pre, mode, res)
+                self._score_phcx(pre, mode, res, slot)
             if pre.pf:
-                self._score_pfd(pre, mode, res)
+                self._score_pfd(pre, mode, res, slot)
         finally:
             pre.close()
         return res
@@ -647,8 +697,9 @@ class DataProcessor:
             self._fail_batch(batch_paths, res)
             _write_progress(out_path, self.start + off + len(batch_paths))
 
-        _stream(paths, run.timed_parse(self._parse), run.timed_score(lambda pre: self._score(pre, mode)),
-                emit, self.batch)
+        _stream(paths, run.timed_parse(self._parse),
+                run.timed_score(lambda pre, slot: self._score(pre, mode, slot)), emit, self.batch,
+                self.depth)
         return counts["ok"], counts["failed"]
 
     # ---- 22 scores / profile bins ---------------------------------------------------
@@ -712,7 +763,8 @@ class DataProcessor:
                     f.write(t)
 
         _stream(paths, run.timed_parse(self._parse),
-                run.timed_score(lambda pre: self._score(pre, "scores")), emit, self.batch)
+                run.timed_score(lambda pre, slot: self._score(pre, "scores", slot)), emit,
+                self.batch, self.depth)
         self._summary(len(paths), counts["ok"], counts["failed"], start, run=run)
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):
@@ -800,7 +852,8 @@ class DataProcessor:
             self._fail_batch(batch_paths, res)
 
         _stream(paths, run.timed_parse(self._parse),
-                run.timed_score(lambda pre: self._score(pre, "label")), emit, self.batch)
+                run.timed_score(lambda pre, slot: self._score(pre, "label", slot)), emit,
+                self.batch, self.depth)
         self._summary(len(paths), counts["ok"], counts["failed"], start,
                       f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n", run=run)
 

@@ -2,7 +2,9 @@
 candidate) against the reference's own 30 values of the same files (tests/golden/
 all30_phcx128.npz, tools/make_golden.py mode "all30"), and the multi-rank path
 (distributed.score_sharded) around the real Engine: two ranks started with spawn, sharing
-cuda:0, gathering over gloo, must reproduce the single-process matrix bit for bit."""
+cuda:0, gathering over gloo, must reproduce the single-process matrix bit for bit; and one
+rank in an RCCL ("nccl") group of one, gathering device tensors with all_gather_into_tensor,
+so the collective the 8-GPU run uses has run on this GPU."""
 import json
 import os
 import socket
@@ -107,3 +109,55 @@ def test_two_ranks_score_sharded_with_engine(engine):
     for r in (0, 1):
         assert res[r].shape == single.shape
         assert np.array_equal(np.nan_to_num(res[r], nan=7.0), np.nan_to_num(single, nan=7.0)), r
+
+
+def _rank_rccl1(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    import torch
+    import torch.distributed as dist
+
+    from pulsarfeatureextractor_amd import distributed as D
+    from pulsarfeatureextractor_amd._native import Engine
+
+    rank, world = D.init_from_env("nccl", group_at_one=True)
+    assert dist.is_initialized() and dist.get_backend() == "nccl" and world == 1
+    d = load("all30_phcx128")
+    arrs = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+            for k, v in zip(("prof", "lyon_dm", "sub", "dmcurve", "scal"), all30_inputs(d))}
+    n = int(arrs["prof"].shape[0])
+    with Engine(0) as eng:
+        def score(prof, lyon_dm, sub, dmcurve, scal):
+            out, st = eng.features30(prof, lyon_dm, sub, dmcurve, scal)
+            eng.synchronize()
+            return torch.cat([out, st.to(torch.float64)[:, None]], dim=1)
+
+        full = D.score_sharded(score, arrs, n)          # RCCL all_gather_into_tensor
+        local = score(**arrs)
+        # an uneven shard layout through the padded path: 3 of the rows as "this rank's"
+        part = D.gather_rows(local[:3].contiguous(), 3)
+    torch.cuda.synchronize()
+    res = (full.device.type, full.cpu().numpy(), local.cpu().numpy(), part.cpu().numpy())
+    q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_group_of_one_gathers_device_matrix(engine):
+    """SURVEY.md 8(e) / north_star's RCCL all-gather: init_from_env("nccl") with WORLD_SIZE = 1
+    and score_sharded / gather_rows over device tensors of the (n, 30) matrix."""
+    import torch.multiprocessing as mp
+
+    d = load("all30_phcx128")
+    out, st = engine.features30(*all30_inputs(d))
+    single = np.concatenate([out, st.astype(np.float64)[:, None]], axis=1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rank_rccl1, args=(_free_port(), q))
+    p.start()
+    dev, full, local, part = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert dev == "cuda"
+    same = lambda a, b: np.array_equal(np.nan_to_num(a, nan=7.0), np.nan_to_num(b, nan=7.0))
+    assert same(full, single) and same(local, single) and same(part, single[:3])

@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--mode", choices=["phases", "stream"], default="phases")
     ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--depth", default="2",
+                    help="GPU pipeline depths to time, comma-separated (DataProcessor gpu_depth)")
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     have = sorted(f for f in os.listdir(args.dir) if f.endswith(".phcx.gz"))
@@ -87,21 +89,30 @@ def main():
             b.close()
         res["reader_parse_pack_files_per_s"] = nfiles / (time.perf_counter() - t0)
         eng = get_engine(0)
-        for kind in ("scores", "dmprof"):
-            out = os.path.join(tempfile.mkdtemp(), "scores.csv")
-            dp = processor.DataProcessor(engine=eng, workers=args.workers, log=lambda *a: None,
-                                         batch=args.batch)
-            t0 = time.perf_counter()
-            if kind == "scores":
-                dp.processPHCXCollectively(args.dir, False, out, False, False, False)
-            else:
-                dp.dmprofPHCX(args.dir, False, out, False, False)
-            wall = time.perf_counter() - t0
-            with open(out) as f:
-                nlines = sum(1 for _ in f)
-            res[kind] = {"wall_s": wall, "files_per_s": nfiles / wall, "lines": nlines}
+        texts = {}
+        for depth in (int(v) for v in args.depth.split(",")):
+            for kind in ("scores", "dmprof"):
+                out = os.path.join(tempfile.mkdtemp(), "scores.csv")
+                dp = processor.DataProcessor(engine=eng, workers=args.workers,
+                                             log=lambda *a: None, batch=args.batch,
+                                             gpu_depth=depth)
+                t0 = time.perf_counter()
+                if kind == "scores":
+                    dp.processPHCXCollectively(args.dir, False, out, False, False, False)
+                else:
+                    dp.dmprofPHCX(args.dir, False, out, False, False)
+                wall = time.perf_counter() - t0
+                with open(out) as f:
+                    text = f.read()
+                same = texts.setdefault(kind, text) == text
+                res[f"{kind}_depth{depth}"] = {"wall_s": wall, "files_per_s": nfiles / wall,
+                                               "lines": text.count("\n"),
+                                               "text_identical_to_first_depth": same,
+                                               "metrics": dp.metrics}
         res["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
-        res["frac_of_reader"] = res["scores"]["files_per_s"] / res["reader_parse_files_per_s"]
+        d0 = args.depth.split(",")[-1]
+        res["frac_of_reader"] = (res[f"scores_depth{d0}"]["files_per_s"] /
+                                 res["reader_parse_pack_files_per_s"])
         print(json.dumps(res))
         return
     eng = get_engine(0)
