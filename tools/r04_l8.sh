@@ -1,4 +1,3 @@
-# round 4: Lyon-8 DataBlock kernel tests + long-row bench, RCCL group-of-one test, e2e stream
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lyon8_gpu.py > gpurun_out/r04_l8_tests.txt 2>&1 && \
