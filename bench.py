@@ -39,7 +39,10 @@ Besides the contract fields the JSON line carries:
                                  + the whole 128 x 128 DataBlock as the DM array (16 KiB rows,
                                  lyon8_u8_pow2), with its HBM roofline
                    lyon8_phcx_ndm120 -- the same with a 120 x 128 DataBlock (15 360-byte
-                                        rows, lyon8_u8_lds)
+                                        rows, lyon8_u8_dm<2>), with its HBM roofline
+                                        and PMC traffic
+                   lyon8_phcx_ndm100 -- an off-set DataBlock length: 100 x 128 (12 800-byte
+                                        rows, lyon8_u8_dm<2>)
 """
 from __future__ import annotations
 
@@ -422,7 +425,10 @@ def run_lyon8(ctx, args, n, lp):
     elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
     bytes_per_launch = n * (lp + args.ld + 8 * 8)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(f"lyon8_u8_{lp}x{args.ld}_n{n}_pmc.json")
+    # HBM bytes per launch: the round-4 PMC passes of this command at the current defaults
+    # (tools/gpu_steps.sh trace_l8 pmc_l8 -> tools/summarize_prof.py); round 2's if absent
+    traffic = (load_traffic(f"r04_lyon8_u8_{lp}x{args.ld}_n{n}.json")
+               or load_traffic(f"lyon8_u8_{lp}x{args.ld}_n{n}_pmc.json"))
     return {
         "metric": "candidates/sec (8-feature path, 128-bin)",
         **common_fields(ctx, n, args.steps, args.warmup, elapsed),
@@ -606,6 +612,22 @@ def tiles_identical(ctx, out, status, blk=16384):
     return same
 
 
+def dm_kernel_name(ld):
+    """The Lyon-8 kernel lyon8.hip's launcher picks for a DataBlock row of ld bytes."""
+    def leaves(n, depth=0):
+        if n <= 128:
+            return [(n, depth)]
+        n2 = n // 2 - (n // 2) % 8
+        return leaves(n2, depth + 1) + leaves(n - n2, depth + 1)
+    nch = (ld + 8191) // 8192
+    lv = leaves(ld - 8192 * (nch - 1))
+    perfect = (len({d for _, d in lv}) == 1 and len(lv) <= 64 and
+               all(64 <= m <= 128 and m % 8 == 0 for m, _ in lv))
+    if ld % 16 == 0 and nch <= 4 and perfect:
+        return f"pfe::lyon8_u8_dm<{nch}>"
+    return "pfe::lyon8_u8_long / lyon8_u8_generic"
+
+
 def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2):
     """The 8 Lyon features at the real PHCX shape (PHCXOperations.getDMCurveData :528-539:
     the Lyon DM array is the whole section-0 DataBlock, nDM x 128 bytes)."""
@@ -622,7 +644,8 @@ def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2)
     per_cand = lp + ld + 8 * 8
     achieved = per_cand * n / (kern_ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC passes of the same shape (tools/summarize_prof.py)
-    traffic = load_traffic(f"r03_lyon8_pow2_{lp}x{ld}_n{n}.json") if ld in (8192, 16384) else None
+    traffic = (load_traffic(f"r03_lyon8_pow2_{lp}x{ld}_n{n}.json") if ld in (8192, 16384)
+               else load_traffic(f"r04_lyon8_dm_{lp}x{ld}_n{n}.json"))
     del prof, dm, out
     return {
         "value": n * ctx.world * steps / elapsed, "unit": "candidates/sec", "steps": steps,
@@ -632,8 +655,7 @@ def run_lyon8_phcx(ctx, args, n=1_000_000, lp=128, ld=16384, steps=10, warmup=2)
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": (f"pfe::lyon8_u8_pow2<{lp}, {ld // 1024}>" if ld in (8192, 16384)
-                                else f"pfe::lyon8_u8_lds<{lp}, 112>" if ld == 15360
-                                else f"pfe::lyon8_u8_lds or lyon8_u8_long<{lp}>"),
+                                else dm_kernel_name(ld)),
                      "algorithmic_bytes_per_candidate": per_cand,
                      "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max},
     }
@@ -768,6 +790,9 @@ def main():
             torch.cuda.empty_cache()
             # nDM = 120 (the golden dmplane's shape): 15 360-byte DataBlock
             extra["lyon8_phcx_ndm120"] = run_lyon8_phcx(ctx, args, ld=15360)
+            torch.cuda.empty_cache()
+            # an nDM outside the round-3 fast set (12 800-byte DataBlock, 72-byte leaves)
+            extra["lyon8_phcx_ndm100"] = run_lyon8_phcx(ctx, args, ld=12800)
     elif args.path == "bates22":
         result, out = run_bates22(ctx, args, n, lp, args.steps, args.warmup)
         if want_cpu:

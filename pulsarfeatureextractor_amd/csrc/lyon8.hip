@@ -717,7 +717,7 @@ __global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ 
 }
 
 // ---- DataBlock rows, round 4: per-byte numpy chains at 4 VALU per byte ------------------
-// lyon8_u8_lds spends ~3.1 k VALU wave-instructions per 15 360-byte row (VALU-bound at 37 %
+// lyon8_u8_lds spent ~3.1 k VALU wave-instructions per 15 360-byte row (VALU-bound at 37 %
 // of HBM): byte extraction from 64-bit words, per-row 128-bit finalisation in every lane,
 // 64-bit wave reductions.  This kernel keeps numpy's arithmetic and removes the rest:
 //   * each byte of a leaf is read from the wave's padded LDS image with ds_read_u8 (the LDS
@@ -730,21 +730,25 @@ __global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ 
 //     finalised once, one row per lane, and stored as one 4 KiB span -- the divisions,
 //     square roots and 128-bit numerators run once per 64 rows instead of once per row;
 //   * each wave owns a contiguous range of rows (no grid-stride tail imbalance).
-// Row layout (numpy): chunks of 8192 values (the first NCH-1 full: 64 leaves of 128), the
-// last chunk a perfect pairwise tree of `leaves` leaves of MW*8 values (host: dm_shape).
-// LDS image: leaf l at l*(m+4) (m+4 = 4 * odd, so the 32 lanes of a ds_read_u8 group hit 32
-// distinct banks), written with ds_write_b32 (the padded stride is only 4-byte aligned).
+// Row layout (numpy's reduction of nDM x 128 values): NCH chunks of 8192, the first NCH-1
+// full (64 leaves of 128), the last one numpy's pairwise tree of <= 64 leaves of 64..128
+// values (multiples of 8) whose leaves all sit at one depth (a perfect binary tree; their
+// lengths may differ, e.g. nDM = 127: 120, 128, 128, 128, ...), so the wave butterfly over
+// lane-ordered leaves is numpy's tree.  That covers every nDM in 3..256 but 33, 97, 161, 225
+// (host: dm_shape).  LDS image per wave: leaf l at l * 132 (132 = 4 * 33: the 32 lanes of a
+// ds_read_u8 group hit 32 distinct banks), written with ds_write_b32 (the padded stride is
+// only 4-byte aligned); the last chunk's 8-byte halves go where a per-block table says.
+constexpr int DM_MAX_LEAVES = 64;
 struct DmShape {
   int lp;          // profile length (64 / 128 / 256)
   int ld;          // DataBlock row length (multiple of 16)
-  int np;          // 1 KiB load instructions per row = ceil(ld / 1024)
   int len_last;    // bytes of the last chunk
   int leaves_last; // leaves of the last chunk (power of two <= 64)
-  uint32_t magic;  // floor(o / m_last) = mulhi(o, magic) for o < 8208
+  uint16_t start[DM_MAX_LEAVES + 1];  // leaf starts of the last chunk (+ its length)
 };
 
-constexpr int DM_S_FULL = 132;
-constexpr int DM_IMG_BYTES = 64 * DM_S_FULL;  // one chunk image per wave (8448 B)
+constexpr int DM_S = 132;                     // LDS leaf stride
+constexpr int DM_IMG_BYTES = 64 * DM_S;       // one chunk image per wave (8448 B)
 
 // 64-lane sum of a 32-bit value: DPP within rows, then the four row sums through the
 // permlane swaps.  Exact; every lane ends with the total.
@@ -759,11 +763,12 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   return b[0] + b[1];
 }
 
-// 8 numpy leaf chains over W words of the leaf at `lb` (LDS), each byte fl(fl(x-mean)^2).
-// The byte reads are volatile so that they stay single ds_read_u8 (zero-extended by the LDS
-// unit) instead of being merged into dword reads that need a VALU extraction per byte.
-template <int W>
-__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean) {
+// numpy's 8 leaf chains over the words k < nw (8..16) of the leaf at lb (LDS): each byte
+// fl(fl(x - mean)^2) added to chain j = i mod 8 in order, then ((r0+r1)+(r2+r3))+((r4+r5)+
+// (r6+r7)).  The byte reads are volatile so that they stay single ds_read_u8 (zero-extended
+// by the LDS unit) instead of being merged into dword reads that need a VALU extraction per
+// byte; words past the leaf are read (inside the image) but not added.
+__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw) {
   typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
   lds_u8* vb = (lds_u8*)lb;
   // software pipeline: the 8 bytes of word k+1 are read while word k is computed
@@ -772,16 +777,18 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean) {
   for (int j = 0; j < 8; ++j) cur[j] = vb[j];
   double r[8];
 #pragma unroll
-  for (int k = 0; k < W; ++k) {
-    if (k + 1 < W) {
+  for (int k = 0; k < 16; ++k) {
+    if (k + 1 < 16) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) nxt[j] = vb[8 * (k + 1) + j];
     }
+    if (k < 8 || k < nw) {  // leaves hold >= 8 words: the first eight need no lane test
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const double d = (double)cur[j] - mean;
-      const double sq = d * d;
-      r[j] = k == 0 ? sq : r[j] + sq;
+      for (int j = 0; j < 8; ++j) {
+        const double d = (double)cur[j] - mean;
+        const double sq = d * d;
+        r[j] = k == 0 ? sq : r[j] + sq;
+      }
     }
     // pin word k's arithmetic before word k+2's reads (empty asm ordered with the volatile
     // reads; without it every read of the leaf is hoisted, one VGPR each)
@@ -793,14 +800,14 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean) {
   return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
 
-// write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image
-template <int NCH, int MW, int NPMAX>
+// write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image.  Full
+// chunks: leaf lane/8 + 8j at offset 16 (lane % 8).  The last chunk: each 8-byte half at the
+// address of the block's table stab (0xFFFF: past the chunk).
+template <int NCH, int NPMAX>
 __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], int ch, int lane,
-                                         uint32_t full_base, const DmShape& sh) {
-  constexpr int ML = 8 * MW;
-  constexpr bool SPLIT = (ML % 16) != 0;  // 16-B pieces straddle two leaves
+                                         uint32_t full_base, const uint16_t* stab) {
   typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;
-  if (ch < NCH - 1) {                     // full chunk: leaf lane/8 + 8j, stride 132
+  if (ch < NCH - 1) {
     // (volatile: single ds_write_b32 with 16-bit immediate offsets from one base register,
     // not ds_write2_b32 pairs whose 8-bit offsets need a base register per piece)
 #pragma unroll
@@ -813,45 +820,48 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
       dst[3] = v.w;
     }
   } else {
-    // recomputed per row (a few VALU) rather than hoisted out of the row loop and spilled
-    uint32_t o0 = 16u * lane;
-    asm volatile("" : "+v"(o0));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t o = o0 + 1024u * j;  // chunk-relative byte offset
-      if (o < (uint32_t)sh.len_last) {  // (pieces of instructions >= np have o >= len_last)
-        const u32x4 v = q[8 * ch + j];
-        const uint32_t a0 = o + 4u * __umulhi(o, sh.magic);
-        if constexpr (SPLIT) {
-          const uint32_t a1 = o + 8u + 4u * __umulhi(o + 8u, sh.magic);
-          reinterpret_cast<uint32_t*>(img + a0)[0] = v.x;
-          reinterpret_cast<uint32_t*>(img + a0)[1] = v.y;
-          reinterpret_cast<uint32_t*>(img + a1)[0] = v.z;
-          reinterpret_cast<uint32_t*>(img + a1)[1] = v.w;
-        } else {
-          uint32_t* dst = reinterpret_cast<uint32_t*>(img + a0);
-          dst[0] = v.x;
-          dst[1] = v.y;
-          dst[2] = v.z;
-          dst[3] = v.w;
-        }
+      const u32x4 v = q[8 * ch + j];
+      const uint32_t a0 = stab[(2 * j) * 64 + lane], a1 = stab[(2 * j + 1) * 64 + lane];
+      if (a0 != 0xFFFFu) {
+        lds_u32* dst = (lds_u32*)(img + a0);
+        dst[0] = v.x;
+        dst[1] = v.y;
+      }
+      if (a1 != 0xFFFFu) {
+        lds_u32* dst = (lds_u32*)(img + a1);
+        dst[0] = v.z;
+        dst[1] = v.w;
       }
     }
   }
 }
 
-template <int NCH, int MW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps,
-                                                   const uint8_t* __restrict__ dm, int64_t ds,
-                                                   int64_t n, double* __restrict__ out,
-                                                   DmShape sh) {
-  static_assert(NCH >= 1 && NCH <= 2 && MW >= 9 && MW <= 16, "shape");
+template <int NCH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : 2, NCH <= 2 ? 4 : 2)))
+void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
+                 int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
+  static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
   constexpr int NPMAX = 8 * NCH;
-  constexpr int ML = 8 * MW;            // leaf length of the last chunk
-  constexpr int SL = ML + 4;            // its LDS leaf stride
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
+  __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
   const int lane = threadIdx.x & 63;
   uint8_t* img = lds[threadIdx.x >> 6];
+  // the block's staging table (row-invariant): half h of lane l's piece j holds chunk bytes
+  // o = 16 l + 1024 j + 8 h, i.e. bytes o - start(L) of leaf L
+  for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {
+    const int jh = e >> 6, l = e & 63;
+    const int o = 16 * l + 1024 * (jh >> 1) + 8 * (jh & 1);
+    uint16_t a = 0xFFFFu;
+    if (o < sh.len_last) {
+      int L = 0;
+      while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
+      a = (uint16_t)(L * DM_S + (o - sh.start[L]));
+    }
+    stab[e] = a;
+  }
+  __syncthreads();
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   // wave-uniform by construction; readfirstlane makes it provable (scalar row loop, SGPR
   // buffer descriptors)
@@ -863,6 +873,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
+  const int nw_last = lane < sh.leaves_last ? (sh.start[lane + 1] - sh.start[lane]) >> 3 : 16;
   for (int64_t base = r0; base < r1; base += 64) {
     const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
     uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
@@ -891,23 +902,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (lane >= ppl) sp = (Acc2){0, 0, 0, 0};
       // ---- numpy's sum of squared deviations, chunk by chunk through the LDS image
       // (chunk 0 is staged before the mean is known, so its registers die early)
-      dm_stage<NCH, MW>(img, q, 0, lane, full_base, sh);
+      dm_stage<NCH>(img, q, 0, lane, full_base, stab);
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
       double ssq = 0.0;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        if (ch > 0) dm_stage<NCH, MW>(img, q, ch, lane, full_base, sh);
+        if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
-        double leaf;
-        if (ch < NCH - 1) {
-          leaf = dm_leaf<16>(img + lane * DM_S_FULL, mean);
-        } else {
-          leaf = dm_leaf<MW>(img + lane * SL, mean);
-          leaf = lane < sh.leaves_last ? leaf : 0.0;
-        }
-        const double cs = wave_sum_f64(leaf);
-        ssq = ch == 0 ? cs : ssq + cs;
+        double leaf = dm_leaf(img + lane * DM_S, mean, ch < NCH - 1 ? 16 : nw_last);
+        if (ch == NCH - 1) leaf = lane < sh.leaves_last ? leaf : 0.0;
+        const double cs = wave_sum_f64(leaf);  // numpy's tree over the lane-ordered leaves
+        ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order
         wave_lds_sync();
       }
       // ---- the other row totals, as exact 32-bit halves
@@ -1068,21 +1074,42 @@ static bool long_row_shape(int ld, LongShape& sh) {
   return false;
 }
 
-// lyon8_u8_dm's layout of a DataBlock row: nch chunks of numpy's reduction, the last one a
-// perfect pairwise tree of <= 64 leaves of 8 * mw bytes (mw in 9..16)
-static bool dm_shape(int lp, int ld, DmShape& sh, int& nch, int& mw) {
-  if (ld <= 256 || ld > 16384 || ld % 16) return false;
+// numpy's pairwise leaves of a contiguous sum of n values (numpy/core pairwise_sum: blocks
+// of <= 128 values; larger ranges split at n/2 rounded down to a multiple of 8): appends
+// (start, length, depth)
+static void np_leaves(int off, int n, int depth, int* start, int* len, int* dep, int& cnt, int cap) {
+  if (n <= 128) {
+    if (cnt < cap) {
+      start[cnt] = off;
+      len[cnt] = n;
+      dep[cnt] = depth;
+    }
+    ++cnt;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  np_leaves(off, n2, depth + 1, start, len, dep, cnt, cap);
+  np_leaves(off + n2, n - n2, depth + 1, start, len, dep, cnt, cap);
+}
+
+// lyon8_u8_dm's layout of a DataBlock row of ld bytes: nch chunks of 8192 values, the last
+// one a perfect pairwise tree (all leaves at one depth) of <= 64 leaves of 64..128 values
+static bool dm_shape(int lp, int ld, DmShape& sh, int& nch) {
+  if (ld <= 256 || ld > 4 * 8192 || ld % 16) return false;
   nch = (ld + 8191) / 8192;
   const int len = ld - 8192 * (nch - 1);
-  int m = 0, leaves = 0;
-  if (!perfect_chunk(len, m, leaves) || leaves > 64 || m % 8) return false;
+  int start[DM_MAX_LEAVES], lens[DM_MAX_LEAVES], dep[DM_MAX_LEAVES], cnt = 0;
+  np_leaves(0, len, 0, start, lens, dep, cnt, DM_MAX_LEAVES);
+  if (cnt > DM_MAX_LEAVES || (cnt & (cnt - 1)) != 0) return false;
+  for (int i = 0; i < cnt; ++i)
+    if (dep[i] != dep[0] || lens[i] % 8 || lens[i] < 64 || lens[i] > 128) return false;
   sh.lp = lp;
   sh.ld = ld;
-  sh.np = (ld + 1023) / 1024;
   sh.len_last = len;
-  sh.leaves_last = leaves;
-  sh.magic = (uint32_t)((0x100000000ull + (uint64_t)m - 1) / (uint64_t)m);
-  mw = m / 8;
+  sh.leaves_last = cnt;
+  for (int i = 0; i < cnt; ++i) sh.start[i] = (uint16_t)start[i];
+  for (int i = cnt; i <= DM_MAX_LEAVES; ++i) sh.start[i] = (uint16_t)len;
   return true;
 }
 
@@ -1104,31 +1131,16 @@ static int resident_blocks() {
   return cached[dev];
 }
 
-template <int NCH, int MW>
+template <int NCH>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dm<NCH, MW>;
+  constexpr auto K = lyon8_u8_dm<NCH>;
   int64_t blocks = resident_blocks<K>();
   const int64_t need = (n + 3) / 4;  // at least one row per wave
   if (blocks > need) blocks = need;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(K, dim3((unsigned)blocks), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
-}
-
-template <int NCH>
-static void launch_dm_mw(int mw, const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
-                         int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  switch (mw) {
-    case 9: launch_dm_kernel<NCH, 9>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 10: launch_dm_kernel<NCH, 10>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 11: launch_dm_kernel<NCH, 11>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 12: launch_dm_kernel<NCH, 12>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 13: launch_dm_kernel<NCH, 13>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 14: launch_dm_kernel<NCH, 14>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    case 15: launch_dm_kernel<NCH, 15>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-    default: launch_dm_kernel<NCH, 16>(prof, ps, dm, ds, n, out, sh, st, cap); break;
-  }
 }
 
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
@@ -1138,14 +1150,16 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
   const bool aligned = ((uintptr_t)prof % 16 == 0) && ((uintptr_t)dm % 16 == 0) &&
                        (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
   DmShape dsh{};
-  int dnch = 0, dmw = 0;
+  int dnch = 0;
   if (o.lyon8_dm == 0 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
-      ld != 16384 && dm_shape(lp, ld, dsh, dnch, dmw)) {
+      ld != 16384 && dm_shape(lp, ld, dsh, dnch)) {
     // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dm
-    if (dnch == 1)
-      launch_dm_mw<1>(dmw, prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks);
-    else
-      launch_dm_mw<2>(dmw, prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks);
+    switch (dnch) {
+      case 1: launch_dm_kernel<1>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
+      case 2: launch_dm_kernel<2>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
+      case 3: launch_dm_kernel<3>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
+      default: launch_dm_kernel<4>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
+    }
     return hipGetLastError();
   }
   if (aligned && lp == ld && (lp == 64 || lp == 128 || lp == 256)) {

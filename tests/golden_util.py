@@ -72,15 +72,49 @@ def envelope_check(out, st, name, skip=(), cols=slice(None)):
     return stats
 
 
+class _Set(dict):
+    """A golden set assembled in memory (same keys as the .npz sets)."""
+
+    @property
+    def files(self):
+        return list(self.keys())
+
+
+def _label_phcx_set():
+    """The PHCX candidates of the --label golden (tests/golden/label.npz) as a bates22 set:
+    inputs phcx_in_*, 'out' = the 22 scores the reference wrote to Scores.csv (Python 3
+    repr, so the golden values are exact), 'ok' = listed in Cands.meta."""
+    g = np.load(os.path.join(GOLDEN, "label.npz"))
+    d = _Set({k[len("phcx_in_"):]: g[k] for k in g.files if k.startswith("phcx_in_")})
+    n = int(d["n"])
+    out = np.full((n, 22), np.nan)
+    ok = np.zeros(n, dtype=bool)
+    for ln in str(g["phcx_Scores.csv"]).splitlines():
+        if not ln:
+            continue
+        vals, name = ln.rsplit(",%", 1)
+        i = int(name.rsplit("label_", 1)[1].split(".")[0])
+        out[i] = [float(v) for v in vals.split(",")[:-1]]
+        ok[i] = True
+    d.update(out=out, ok=ok, superb=np.bool_(False))
+    return d
+
+
 def load(name):
+    if name == "label_phcx":
+        return _label_phcx_set()
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 
 
 def bates_inputs(d):
     """Arrays in the libpfe layout from a bates22 golden set."""
     superb = bool(d["superb"])
-    blk = d["block0"] if superb else d["block1"]
-    curves = np.stack([reduce_dm_curve(b)[0] for b in blk])
+    if "dmcurve" in d.files:  # compact sets store the reduced curves and the block length
+        curves, blen = d["dmcurve"], int(d["block_len"])
+    else:
+        blk = d["block0"] if superb else d["block1"]
+        curves = np.stack([reduce_dm_curve(b)[0] for b in blk])
+        blen = blk.shape[1]
     n = len(d["ok"])
     scal = np.zeros((n, 8))
     scal[:, 0] = d["period"] * 1000
@@ -89,7 +123,7 @@ def bates_inputs(d):
     scal[:, 3] = d["width"]
     scal[:, 4] = d["dm_start"]
     scal[:, 5] = d["dm_end"]
-    scal[:, 6] = blk.shape[1]
+    scal[:, 6] = blen
     return d["prof"], d["sub"], curves, scal
 
 

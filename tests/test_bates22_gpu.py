@@ -115,10 +115,32 @@ def test_vs_reference_golden(engine, name):
     envelope_check(out, st, name, skip=BITEXACT)
 
 
+@pytest.mark.parametrize("name", ["bates22_phcx128_big", "bates22_superb64_big"])
+def test_vs_reference_golden_big(engine, name):
+    """1000 PHCX / 500 SUPERB candidates scored by the reference itself (round 4): the same
+    failing candidates, the bit-exact columns exact, and every LM score pinned row by row to
+    the reference's own 50-sample envelope (tight rows inside, chaotic rows to the binomial
+    bound) -- many more tight rows for s10/s11/s17/s18 than the 300 / 150-row sets."""
+    d = load(name)
+    prof, sub, curve, scal = bates_inputs(d)
+    out, st = engine.bates22(prof, sub, curve, scal)
+    assert not (st & 0x10).any(), "PFE_ST_UNSUPPORTED"
+    gok = (st & 0xFF) == 0
+    assert np.array_equal(gok, d["ok"].astype(bool)), f"{name}: failure pattern differs"
+    r = rel_err(out[gok], d["out"][gok])
+    for j in BITEXACT:
+        assert (r[:, j] == 0).all(), f"{name}: s{j + 1} not bit-exact ({(r[:, j] > 0).sum()} rows)"
+    stats = envelope_check(out, st, name, skip=BITEXACT)
+    for sc in (10, 11, 17, 18):
+        assert stats[sc][0] >= 100, f"{name}: only {stats[sc][0]} tight rows for s{sc}"
+
+
 def test_vs_oracle_fresh_inputs(engine):
-    b = bates_batch(160, seed=77)
+    """1000 fresh candidates against the oracle (eight oracle passes in 8 spawned processes)."""
+    b = bates_batch(1000, seed=77)
     out, st = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
-    ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    ref, rst, own, rmax = oracle_with_floor(b["prof"], b["sub"], b["dmcurve"], b["scal"],
+                                            workers=8)
     gold = FLOOR["bates22_phcx128"]
     floor = {k: np.maximum(own[k], gold[k]).tolist() for k in gold if k.startswith("moved")}
     check_against(out, st, ref, (rst & 0xFF) == 0, "oracle", floor, rmax=rmax)

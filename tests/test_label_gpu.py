@@ -17,7 +17,7 @@ import sys
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN, load
+from golden_util import GOLDEN, envelope_check, load
 from pulsarfeatureextractor_amd import cli, pfd, phcx
 from pulsarfeatureextractor_amd._native import Engine
 from test_pfd22_gpu import check as pfd_check
@@ -95,10 +95,19 @@ def test_label_phcx(tmp_path, monkeypatch):
         k = f"<DIR>/label_{i:05d}.phcx.gz"
         if k in o:
             assert [py2_str(v) for v in sc[i]] == [py2_str(v) for v in o[k]], k
-    # ... and the columns that are bit-exact against the reference agree with its file
+    # ... the columns that are bit-exact against the reference agree with its file
     for k in r:
         for j in (2, 3, 11, 12, 13, 14, 15, 19, 21):
             assert float("%.12g" % r[k][j]) == o[k][j], (k, j)
+    # ... and the LM columns of the file lie in the reference's own per-row envelope of the
+    # same candidates (tools/chaos_envelope.py set "label_phcx")
+    text = np.full((n, 22), np.nan)
+    tst = np.ones(n, dtype=np.uint32)
+    for i in range(n):
+        k = f"<DIR>/label_{i:05d}.phcx.gz"
+        if k in o:
+            text[i], tst[i] = o[k], 0
+    envelope_check(text, tst, "label_phcx", skip=(2, 3, 11, 12, 13, 14, 15, 19, 21))
 
 
 def test_label_pfd(tmp_path, monkeypatch):

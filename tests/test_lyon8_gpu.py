@@ -109,7 +109,7 @@ def test_long_dm_rows_vs_oracle(engine, lp, ld):
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
-@pytest.mark.parametrize("ld", [15360, 12800, 9216])
+@pytest.mark.parametrize("ld", [15360, 12800, 9216, 16256, 30720])
 def test_long_dm_rows_multibatch(engine, ld):
     """lyon8_u8_dm with one block (4 waves) over 600 rows: every wave runs several batches of
     up to 64 rows (finalised one row per lane), the last one partial.  Bit-identical to the
@@ -136,11 +136,23 @@ def test_long_dm_rows_kernel_options_agree(engine):
     assert (np.abs(a - b)[m] / np.maximum(1, np.abs(b[m]))).max() <= TOL
 
 
-@pytest.mark.parametrize("ld", [16256, 4352, 30720])
+@pytest.mark.parametrize("ld", [16256, 4352, 30720, 24576, 6272])
 def test_long_dm_rows_other_lengths(engine, ld):
-    """DataBlock lengths whose numpy pairwise trees are not perfect (nDM = 127, 34, 240):
-    the generic kernel, exact rational moments -- means bit-exact, the rest within 1e-12."""
+    """DataBlock lengths outside the round-3 fast set, all through lyon8_u8_dm (round 4):
+    nDM = 127 / 34 / 49 (the last chunk's leaves differ in length -- 120 and 128, 64 and 72,
+    96 and 104 -- on a perfect tree), 240 / 192 (four and three numpy chunks) -- mean and std
+    bit-exact, skew/kurt within 1e-12."""
     prof, dm = lyon_batch(200, 128, ld, seed=7 + ld, adversarial=True)
+    got = engine.lyon8(prof, dm)
+    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
+
+
+@pytest.mark.parametrize("ld", [4224, 12416, 20608])
+def test_long_dm_rows_imperfect_trees(engine, ld):
+    """nDM = 33 / 97 / 161: three of the four DataBlock lengths <= 256 rows whose numpy tree is
+    not perfect (leaves at two depths): the round-3 kernels (lyon8_u8_long / generic), exact
+    rational moments -- means bit-exact, the rest within 1e-12."""
+    prof, dm = lyon_batch(200, 128, ld, seed=9 + ld, adversarial=True)
     got = engine.lyon8(prof, dm)
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4))
 

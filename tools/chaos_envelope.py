@@ -40,7 +40,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide")
+SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide",
+        "bates22_phcx128_big", "bates22_superb64_big", "label_phcx")
 # the unperturbed oracle, start points +-1..+-4 ulp, 40 residual patterns: with the golden
 # value, K = 50 samples of the reference's own spread per candidate
 PERTS = (0, 1, -1, 2, -2, 3, -3, 4, -4) + tuple(f"r{s}" for s in range(101, 141))
@@ -87,23 +88,27 @@ def envelope(results, golden, gold_ok):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--sets", default=",".join(SETS),
+                    help="comma-separated sets to (re)compute; the others keep their envelopes")
     args = ap.parse_args()
     from golden_util import load
 
-    jobs = [(s, p) for s in SETS for p in PERTS]
-    by_set = {s: [] for s in SETS}
+    sets = [s for s in args.sets.split(",") if s]
+    jobs = [(s, p) for s in sets for p in PERTS]
+    by_set = {s: [] for s in sets}
     with ProcessPoolExecutor(args.workers) as ex:
         for name, pert, res in ex.map(_run, jobs):
             by_set[name].append(res)
             print(name, pert, "done", flush=True)
-    out = {}
-    for s in SETS:
+    path = os.path.join(ROOT, "tests", "golden", "chaos_envelope.npz")
+    out = dict(np.load(path)) if os.path.exists(path) else {}
+    for s in sets:
         d = load(s)
         golden = d["out"][:, -22:]
         lo, hi, fixed = envelope(by_set[s], golden, d["ok"].astype(bool))
         out[f"{s}_lo"], out[f"{s}_hi"], out[f"{s}_fixed"] = lo, hi, fixed
     out["runs"] = np.array([str(p) for p in PERTS])
-    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "chaos_envelope.npz"), **out)
+    np.savez_compressed(path, **out)
 
 
 if __name__ == "__main__":

@@ -248,7 +248,12 @@ SPECS = [
     # near-flat profiles quantised from sigma ~ 0.5 noise under a narrow pulse: tiny
     # interquartile ranges, so Freedman-Diaconis histograms of 1000-1600 bins (rows 8..39)
     ("bates22_phcx128_wide", "bates22", False, 48, 128, 128, 16, 128, 128, 9),
+    # round 4: larger sets for the per-row envelope pins of the chaotic LM scores (more tight
+    # rows for s10/s11/s17/s18); stored with the reduced DM curves instead of the DataBlocks
+    ("bates22_phcx128_big", "bates22", False, 1000, 128, 128, 16, 128, 128, 11),
+    ("bates22_superb64_big", "bates22", True, 500, 64, 64, 16, 64, 120, 12),
 ]
+COMPACT = ("bates22_phcx128_big", "bates22_superb64_big")
 
 
 def lownoise_wide_rows(rng, n, lp):
@@ -311,11 +316,18 @@ def main(only=None):
             res = run_reference(refdir, files, mode, tmp)
             nout = {"lyon8": 8, "bates22": 22, "all30": 30}[mode]
             out, ok, errs = collect(res, nout)
+            blocks_kw = dict(block0=np.asarray(arrays["block0"]).astype(np.uint8),
+                             block1=np.asarray(arrays["block1"]).astype(np.uint8))
+            if name in COMPACT:  # the scored section's reduced DM curve instead of the blocks
+                from pulsarfeatureextractor_amd.phcx import reduce_dm_curve
+
+                fit_blk = np.asarray(arrays["block0"] if superb else arrays["block1"])
+                blocks_kw = dict(dmcurve=np.stack([reduce_dm_curve(b)[0] for b in fit_blk]),
+                                 block_len=int(fit_blk.shape[1]))
             np.savez_compressed(
                 os.path.join(GOLDEN, name + ".npz"),
                 prof=arrays["prof"].astype(np.uint8), sub=arrays["sub"].astype(np.uint8),
-                block0=np.asarray(arrays["block0"]).astype(np.uint8),
-                block1=np.asarray(arrays["block1"]).astype(np.uint8),
+                **blocks_kw,
                 period=arrays["period"], dm=arrays["dm"], snr=arrays["snr"],
                 width=arrays["width"], dm_start=arrays["dm_start"], dm_end=arrays["dm_end"],
                 n_dm_index=arrays["n_dm_index"], superb=superb, out=out, ok=ok, err=errs)
