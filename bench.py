@@ -130,14 +130,22 @@ def cpu_baseline_lyon8(lp, ld, sample):
         t0 = time.perf_counter()
         lyon8(prof, dm)
         dt = time.perf_counter() - t0
+    value = sample / dt
+    survey = 736.0  # candidates/s through the reference's own objects
+    ratio = value / survey
     return {
-        "value": sample / dt, "unit": "candidates/sec", "cores": 1, "kind": "port",
+        "value": value, "unit": "candidates/sec", "cores": 1, "kind": "port",
         "sample": f"{sample} synthetic {lp}-bin profile + {ld}-bin DM rows through the "
                   f"reference-equivalent per-candidate numpy.mean/std + scipy.stats.skew/"
                   f"kurtosis loop (oracle.lyon.lyon8), {dt:.1f} s on 1 host core",
-        "note": "the per-candidate statistics only: the reference's own path also parses each "
-                "PHCX file (SURVEY.md §8(d) measured 736 candidates/s through its objects), so "
-                "this baseline is the faster of the two",
+        "survey_reference_rate": survey,
+        "ratio_to_survey": ratio,
+        "within_2x_of_survey": bool(0.5 <= ratio <= 2.0),
+        "note": ("OUTSIDE SURVEY.md §8(d)(i)'s 2x window: " if not 0.5 <= ratio <= 2.0 else "") +
+                "the per-candidate statistics only; the reference's own path also builds a "
+                "Candidate object and parses each PHCX file per candidate (736 candidates/s in "
+                "the survey), so this baseline is the faster of the two and the GPU/CPU ratio "
+                "it implies is the conservative one",
     }
 
 

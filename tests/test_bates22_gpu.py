@@ -198,6 +198,26 @@ def test_batched_solver_matches_wave_solver(engine):
     lm_columns_agree(o0, s0, o1, s1, floor_for(128), tag="wave vs batched")
 
 
+@pytest.mark.parametrize("solver", ["wave", "batched"])
+def test_every_solver_inside_reference_envelope(engine, solver):
+    """The determinism guard between the GPU solvers that the FMA-contracted linear algebra
+    took from bit identity: each non-default solver, like the pooled default
+    (test_vs_reference_golden), holds every tight row of the reference's own 50-sample
+    envelope and the binomial bound on the chaotic rows, with the bit-exact columns exact --
+    so a real divergence in one solver fails on the rows where the reference is
+    reproducible, with no slack."""
+    d = load("bates22_phcx128")
+    prof, sub, curve, scal = bates_inputs(d)
+    with engine.options(solver=solver):
+        out, st = engine.bates22(prof, sub, curve, scal)
+    gok = (st & 0xFF) == 0
+    assert np.array_equal(gok, d["ok"].astype(bool)), solver
+    r = rel_err(out[gok], d["out"][gok])
+    for j in BITEXACT:
+        assert (r[:, j] == 0).all(), f"{solver}: s{j + 1}"
+    envelope_check(out, st, "bates22_phcx128", skip=BITEXACT)
+
+
 def test_concurrent_groups_and_hand_over_bit_identical(engine):
     """The score groups on side streams (default) vs in order on one stream (option
     serial=1), the LM hand-over of accepted residuals (default) vs re-evaluation
