@@ -116,8 +116,9 @@ int pfe_synchronize(pfe_handle* h);
  *   PFE_OPT_PFD_WAVES    waves per fold of the PFD preprocessing kernel: 4 (default) or 1
  *   PFE_OPT_LYON8_DM     (bits) Lyon-8 kernel for DataBlock-length DM rows (PHCX nDM x 128
  *                        bytes): 0 = per-byte LDS kernel with batched finalisation (default),
- *                        1 = the round-3 kernels.  Mean and std are numpy's bits either way;
- *                        skew / kurt may differ in the last bits (scipy's m2 vs the exact one)
+ *                        1 = the round-3 kernels, 2 = as 0 with skew / kurt from fp64 d^3 / d^4
+ *                        sums (A/B).  Mean and std are numpy's bits either way; skew / kurt
+ *                        may differ in the last bits (scipy's m2 vs the exact one)
  * Returns PFE_EINVAL for an unknown option or an out-of-range value.
  * --------------------------------------------------------------------------------------- */
 #define PFE_OPT_SOLVER 1

@@ -768,7 +768,9 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // (r6+r7)).  The byte reads are volatile so that they stay single ds_read_u8 (zero-extended
 // by the LDS unit) instead of being merged into dword reads that need a VALU extraction per
 // byte; words past the leaf are read (inside the image) but not added.
-__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw) {
+template <bool FPM>
+__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw, double& a3,
+                                          double& a4) {
   typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
   lds_u8* vb = (lds_u8*)lb;
   // software pipeline: the 8 bytes of word k+1 are read while word k is computed
@@ -776,6 +778,9 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw
 #pragma unroll
   for (int j = 0; j < 8; ++j) cur[j] = vb[j];
   double r[8];
+  // FPM: scipy's d^3 = d^2 * d and d^4 = (d^2)^2 terms, fused into running sums per lane
+  // (two accumulators each, any order: only numpy's d^2 sum is held to numpy's order)
+  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     if (k + 1 < 16) {
@@ -788,15 +793,22 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw
         const double d = (double)cur[j] - mean;
         const double sq = d * d;
         r[j] = k == 0 ? sq : r[j] + sq;
+        if constexpr (FPM) {
+          c3[j & 1] = __builtin_fma(sq, d, c3[j & 1]);
+          c4[j & 1] = __builtin_fma(sq, sq, c4[j & 1]);
+        }
       }
     }
     // pin word k's arithmetic before word k+2's reads (empty asm ordered with the volatile
     // reads; without it every read of the leaf is hoisted, one VGPR each)
     asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
                  "+v"(r[6]), "+v"(r[7]));
+    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
 #pragma unroll
     for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
   }
+  a3 = c3[0] + c3[1];
+  a4 = c4[0] + c4[1];
   return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
 
@@ -838,7 +850,9 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
   }
 }
 
-template <int NCH>
+// FPM (PFE_OPT_LYON8_DM = 2, A/B): skew / kurt from fp64 d^3 / d^4 sums fused into the byte
+// loop (2 FMAs per byte) instead of the exact integer power sums (3 packed ops per byte)
+template <int NCH, bool FPM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : 2, NCH <= 2 ? 4 : 2)))
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
@@ -893,10 +907,20 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       // ---- exact power sums of the DM row; a zero byte past the row adds y^3 = -2^21 and
       // y^4 = 2^28 (y = x - 128) and nothing to sum x, sum x^2
       Acc2 sd = {0, 0, 0, 0};
+      if constexpr (FPM) {
 #pragma unroll
-      for (int k = 0; k < NPMAX; ++k) acc2_x4(q[k], sd);
-      sd.t3 += zpad << 21;
-      sd.t4 -= (uint64_t)zpad << 28;
+        for (int k = 0; k < NPMAX; ++k) {
+          sd.s1 = __builtin_amdgcn_udot4(q[k].x, 0x01010101u, sd.s1, false);
+          sd.s1 = __builtin_amdgcn_udot4(q[k].y, 0x01010101u, sd.s1, false);
+          sd.s1 = __builtin_amdgcn_udot4(q[k].z, 0x01010101u, sd.s1, false);
+          sd.s1 = __builtin_amdgcn_udot4(q[k].w, 0x01010101u, sd.s1, false);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NPMAX; ++k) acc2_x4(q[k], sd);
+        sd.t3 += zpad << 21;
+        sd.t4 -= (uint64_t)zpad << 28;
+      }
       Acc2 sp = {0, 0, 0, 0};  // (every lane, no branch: a branch here drains vmcnt)
       acc2_x4(pq, sp);
       if (lane >= ppl) sp = (Acc2){0, 0, 0, 0};
@@ -905,23 +929,43 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       dm_stage<NCH>(img, q, 0, lane, full_base, stab);
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
-      double ssq = 0.0;
+      double ssq = 0.0, a3 = 0.0, a4 = 0.0;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
-        double leaf = dm_leaf(img + lane * DM_S, mean, ch < NCH - 1 ? 16 : nw_last);
-        if (ch == NCH - 1) leaf = lane < sh.leaves_last ? leaf : 0.0;
+        double l3, l4;
+        double leaf = dm_leaf<FPM>(img + lane * DM_S, mean, ch < NCH - 1 ? 16 : nw_last, l3, l4);
+        if (ch == NCH - 1) {
+          const bool in = lane < sh.leaves_last;
+          leaf = in ? leaf : 0.0;
+          l3 = in ? l3 : 0.0;
+          l4 = in ? l4 : 0.0;
+        }
+        a3 += l3;
+        a4 += l4;
         const double cs = wave_sum_f64(leaf);  // numpy's tree over the lane-ordered leaves
         ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order
         wave_lds_sync();
       }
-      // ---- the other row totals, as exact 32-bit halves
-      const uint32_t S2 = wave_sum_u32(sd.s2);
-      const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
-      const uint32_t T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
-      const uint32_t T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
-      const uint32_t T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
+      // ---- the other row totals, as exact 32-bit halves (FPM: the fp64 d^3 / d^4 sums,
+      // parked as their two 32-bit halves)
+      uint32_t S2, T3l, T3h, T4l, T4h;
+      if constexpr (FPM) {
+        const uint64_t b3 = (uint64_t)__double_as_longlong(wave_sum_f64(a3));
+        const uint64_t b4 = (uint64_t)__double_as_longlong(wave_sum_f64(a4));
+        S2 = 0;
+        T3l = (uint32_t)b3;
+        T3h = (uint32_t)(b3 >> 32);
+        T4l = (uint32_t)b4;
+        T4h = (uint32_t)(b4 >> 32);
+      } else {
+        S2 = wave_sum_u32(sd.s2);
+        T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
+        T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
+        T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
+        T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
+      }
       const uint32_t P1 = (uint32_t)group_sum_i32<16>((int)sp.s1);
       const uint32_t P2 = (uint32_t)group_sum_i32<16>((int)sp.s2);
       const uint32_t P3 = (uint32_t)group_sum_i32<16>(sp.t3);
@@ -958,12 +1002,19 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       // third / fourth moments over scipy's m2 = ssq / n
       const long long D = sh.ld;
       const long long S1 = (long long)kS1;
-      const long long T1 = S1 - 128ll * D;
-      const long long T2 = (long long)kS2 - 256ll * S1 + 16384ll * D;
-      const long long T3 = (long long)(int)kT3h * 65536ll + (long long)kT3l;
-      const uint64_t T4 = ((uint64_t)kT4h << 24) + (uint64_t)kT4l;
-      const Moments md = moments_i128(D, T1, T2, T3, T4);
       const double dn = (double)D;
+      Moments md;
+      if constexpr (FPM) {
+        md.mean = (double)S1 / dn;
+        md.m3 = __longlong_as_double((long long)(((uint64_t)kT3h << 32) | kT3l)) / dn;
+        md.m4 = __longlong_as_double((long long)(((uint64_t)kT4h << 32) | kT4l)) / dn;
+      } else {
+        const long long T1 = S1 - 128ll * D;
+        const long long T2 = (long long)kS2 - 256ll * S1 + 16384ll * D;
+        const long long T3 = (long long)(int)kT3h * 65536ll + (long long)kT3l;
+        const uint64_t T4 = ((uint64_t)kT4h << 24) + (uint64_t)kT4l;
+        md = moments_i128(D, T1, T2, T3, T4);
+      }
       const double m2 = kssq / dn;
       const double e = 2.220446049250313e-16 * md.mean;
       const bool zd = m2 <= e * e;
@@ -1131,10 +1182,10 @@ static int resident_blocks() {
   return cached[dev];
 }
 
-template <int NCH>
+template <int NCH, bool FPM>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dm<NCH>;
+  constexpr auto K = lyon8_u8_dm<NCH, FPM>;
   int64_t blocks = resident_blocks<K>();
   const int64_t need = (n + 3) / 4;  // at least one row per wave
   if (blocks > need) blocks = need;
@@ -1151,14 +1202,22 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
                        (ps % 16 == 0) && (ds % 16 == 0) && ((uintptr_t)out % 16 == 0);
   DmShape dsh{};
   int dnch = 0;
-  if (o.lyon8_dm == 0 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
+  if (o.lyon8_dm != 1 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
       ld != 16384 && dm_shape(lp, ld, dsh, dnch)) {
     // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dm
+    const int cap = o.lyon8_blocks;
+    if (o.lyon8_dm == 2 && dnch <= 2) {  // A/B: fp64 d^3 / d^4 moments
+      if (dnch == 1)
+        launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
+      else
+        launch_dm_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
+      return hipGetLastError();
+    }
     switch (dnch) {
-      case 1: launch_dm_kernel<1>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
-      case 2: launch_dm_kernel<2>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
-      case 3: launch_dm_kernel<3>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
-      default: launch_dm_kernel<4>(prof, ps, dm, ds, n, out, dsh, st, o.lyon8_blocks); break;
+      case 1: launch_dm_kernel<1, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+      case 2: launch_dm_kernel<2, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+      case 3: launch_dm_kernel<3, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+      default: launch_dm_kernel<4, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
     }
     return hipGetLastError();
   }

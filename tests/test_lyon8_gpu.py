@@ -122,18 +122,21 @@ def test_long_dm_rows_multibatch(engine, ld):
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
-def test_long_dm_rows_kernel_options_agree(engine):
-    """The round-3 DataBlock kernels (PFE_OPT_LYON8_DM = 1) and lyon8_u8_dm give the same
-    mean/std bits; skew/kurt agree to 1e-12 (scipy's m2 vs the exact one)."""
+@pytest.mark.parametrize("opt", [1, 2])
+def test_long_dm_rows_kernel_options_agree(engine, opt):
+    """The round-3 DataBlock kernels (PFE_OPT_LYON8_DM = 1) and the fp64-moment A/B variant
+    of lyon8_u8_dm (= 2) against the default: the same mean/std bits; skew/kurt agree to
+    1e-12, and the variant is held to the oracle like the default."""
     prof, dm = lyon_batch(400, 128, 15360, seed=77, adversarial=True)
     a = engine.lyon8(prof, dm)
-    with engine.options(lyon8_dm=1):
+    with engine.options(lyon8_dm=opt):
         b = engine.lyon8(prof, dm)
     for c in (0, 1, 4, 5):
         assert np.array_equal(a[:, c], b[:, c], equal_nan=True)
     m = ~np.isnan(b)
     assert np.array_equal(np.isnan(a), np.isnan(b))
     assert (np.abs(a - b)[m] / np.maximum(1, np.abs(b[m]))).max() <= TOL
+    check(b, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
 @pytest.mark.parametrize("ld", [16256, 4352, 30720, 24576, 6272])
