@@ -131,8 +131,11 @@ def test_vs_reference_golden_big(engine, name):
     for j in BITEXACT:
         assert (r[:, j] == 0).all(), f"{name}: s{j + 1} not bit-exact ({(r[:, j] > 0).sum()} rows)"
     stats = envelope_check(out, st, name, skip=BITEXACT)
-    for sc in (10, 11, 17, 18):
-        assert stats[sc][0] >= 100, f"{name}: only {stats[sc][0]} tight rows for s{sc}"
+    # the reference is reproducible (tight) on 367 / 97 rows of the PHCX set and 48 / 51 of
+    # the SUPERB set for s10-s11 / s17-s18 (tools/chaos_envelope.py): all of them were checked
+    least = {"bates22_phcx128_big": (360, 90), "bates22_superb64_big": (45, 45)}[name]
+    for sc, k in ((10, 0), (11, 0), (17, 1), (18, 1)):
+        assert stats[sc][0] >= least[k], f"{name}: only {stats[sc][0]} tight rows for s{sc}"
 
 
 def test_vs_oracle_fresh_inputs(engine):

@@ -32,7 +32,8 @@ def test_lyon8_oracle_bit_exact(name):
 
 
 @pytest.mark.parametrize("name,rows", [("bates22_phcx128", 90), ("bates22_superb64", 45),
-                                       ("bates22_phcx128_wide", 20)])
+                                       ("bates22_phcx128_wide", 20),
+                                       ("bates22_phcx128_big", 40), ("bates22_superb64_big", 30)])
 def test_bates22_oracle_vs_reference(name, rows):
     d = load(name)
     prof, sub, curve, scal = bates_inputs(d)
