@@ -765,32 +765,36 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 
 // numpy's 8 leaf chains over the words k < nw (8..16) of the leaf at lb (LDS): each byte
 // fl(fl(x - mean)^2) added to chain j = i mod 8 in order, then ((r0+r1)+(r2+r3))+((r4+r5)+
-// (r6+r7)).  The byte reads are volatile so that they stay single ds_read_u8 (zero-extended
-// by the LDS unit) instead of being merged into dword reads that need a VALU extraction per
-// byte; words past the leaf are read (inside the image) but not added.
+// (r6+r7)).  Three VALU per byte, all of numpy's roundings kept, in a scaled domain:
+//   * the byte is read with ds_read_u8 (volatile, so it stays one zero-extended byte per read
+//     instead of a dword that needs a VALU extraction per byte) into the low half of a VGPR
+//     pair whose high half is a zero kept in a register for the whole kernel (z[j]); the pair
+//     read as a double is the denormal x * 2^-1074 (fp64 denormals are not flushed:
+//     .amdhsa_float_denorm_mode_16_64 3);
+//   * d' = fma(2^1023, X, -mean * 2^-51) = fl(x - mean) * 2^-51: the product is exact and
+//     the one rounding is the rounding of x - mean, scaled by a power of two (no conversion,
+//     no separate subtraction);
+//   * sq' = d' * d' = fl(d^2) * 2^-102 and every chain sum likewise (all values stay normal),
+//     so the leaf sum is numpy's times 2^-102 exactly (the caller scales it back).
+// FPM adds scipy's d^3 = d^2 * d and d^4 = (d^2)^2 as fused running sums (scaled 2^-153 and
+// 2^-204), in any order.  Words past the leaf (k >= nw) are read inside the image, not added.
 template <bool FPM>
-__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw, double& a3,
-                                          double& a4) {
+__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double nm, double sc,
+                                          const uint32_t (&z)[8], int nw, double& a3, double& a4) {
   typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
   lds_u8* vb = (lds_u8*)lb;
-  // software pipeline: the 8 bytes of word k+1 are read while word k is computed
-  uint32_t cur[8], nxt[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) cur[j] = vb[j];
   double r[8];
-  // FPM: scipy's d^3 = d^2 * d and d^4 = (d^2)^2 terms, fused into running sums per lane
-  // (two accumulators each, any order: only numpy's d^2 sum is held to numpy's order)
   double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (k + 1 < 16) {
+    uint32_t x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) nxt[j] = vb[8 * (k + 1) + j];
-    }
+    for (int j = 0; j < 8; ++j) x[j] = vb[8 * k + j];
     if (k < 8 || k < nw) {  // leaves hold >= 8 words: the first eight need no lane test
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const double d = (double)cur[j] - mean;
+        const double X = __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]);
+        const double d = __builtin_fma(sc, X, nm);
         const double sq = d * d;
         r[j] = k == 0 ? sq : r[j] + sq;
         if constexpr (FPM) {
@@ -799,13 +803,11 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double mean, int nw
         }
       }
     }
-    // pin word k's arithmetic before word k+2's reads (empty asm ordered with the volatile
+    // pin word k's arithmetic before word k+1's reads (empty asm ordered with the volatile
     // reads; without it every read of the leaf is hoisted, one VGPR each)
     asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
                  "+v"(r[6]), "+v"(r[7]));
     if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
   }
   a3 = c3[0] + c3[1];
   a4 = c4[0] + c4[1];
@@ -888,6 +890,16 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
   const int nw_last = lane < sh.leaves_last ? (sh.start[lane + 1] - sh.start[lane]) >> 3 : 16;
+  // dm_leaf's constants: eight zeros held in registers (the high halves of the byte pairs)
+  // and 2^1023 in an SGPR pair (a VOP3 operand; as a literal it would cost a move per byte)
+  uint32_t z[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    z[j] = 0u;
+    asm volatile("" : "+v"(z[j]));
+  }
+  double sc = 0x1p1023;
+  asm volatile("" : "+s"(sc));
   for (int64_t base = r0; base < r1; base += 64) {
     const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
     uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
@@ -929,13 +941,14 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       dm_stage<NCH>(img, q, 0, lane, full_base, stab);
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
+      const double nm = -__builtin_ldexp(mean, -51);  // exact
       double ssq = 0.0, a3 = 0.0, a4 = 0.0;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
         double l3, l4;
-        double leaf = dm_leaf<FPM>(img + lane * DM_S, mean, ch < NCH - 1 ? 16 : nw_last, l3, l4);
+        double leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
           const bool in = lane < sh.leaves_last;
           leaf = in ? leaf : 0.0;
@@ -945,9 +958,12 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         a3 += l3;
         a4 += l4;
         const double cs = wave_sum_f64(leaf);  // numpy's tree over the lane-ordered leaves
-        ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order
+        ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order (all scaled by 2^-102)
         wave_lds_sync();
       }
+      ssq = __builtin_ldexp(ssq, 102);  // exact: numpy's sum of squared deviations
+      a3 = __builtin_ldexp(a3, 153);
+      a4 = __builtin_ldexp(a4, 204);
       // ---- the other row totals, as exact 32-bit halves (FPM: the fp64 d^3 / d^4 sums,
       // parked as their two 32-bit halves)
       uint32_t S2, T3l, T3h, T4l, T4h;
