@@ -942,6 +942,34 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
       const double nm = -__builtin_ldexp(mean, -51);  // exact
+      // ---- the integer row totals (exact 32-bit halves) are reduced and parked in lane i
+      // now, so their registers are free during the byte loop; profile sums: row 0's
+      const bool mine = lane == i;
+      if constexpr (!FPM) {
+        const uint32_t S2 = wave_sum_u32(sd.s2);
+        const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
+        const uint32_t T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
+        const uint32_t T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
+        const uint32_t T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
+        kS2 = mine ? S2 : kS2;
+        kT3l = mine ? T3l : kT3l;
+        kT3h = mine ? T3h : kT3h;
+        kT4l = mine ? T4l : kT4l;
+        kT4h = mine ? T4h : kT4h;
+      }
+      {
+        const uint32_t P1 = (uint32_t)group_sum_i32<16>((int)sp.s1);
+        const uint32_t P2 = (uint32_t)group_sum_i32<16>((int)sp.s2);
+        const uint32_t P3 = (uint32_t)group_sum_i32<16>(sp.t3);
+        const uint32_t P4l = (uint32_t)group_sum_i32<16>((int)(sp.t4 & 0xFFFFFFu));
+        const uint32_t P4h = (uint32_t)group_sum_i32<16>((int)(sp.t4 >> 24));
+        kS1 = mine ? S1 : kS1;
+        kP1 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P1) : kP1;
+        kP2 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P2) : kP2;
+        kP3 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P3) : kP3;
+        kP4l = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4l) : kP4l;
+        kP4h = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4h) : kP4h;
+      }
       double ssq = 0.0, a3 = 0.0, a4 = 0.0;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
@@ -962,44 +990,14 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         wave_lds_sync();
       }
       ssq = __builtin_ldexp(ssq, 102);  // exact: numpy's sum of squared deviations
-      a3 = __builtin_ldexp(a3, 153);
-      a4 = __builtin_ldexp(a4, 204);
-      // ---- the other row totals, as exact 32-bit halves (FPM: the fp64 d^3 / d^4 sums,
-      // parked as their two 32-bit halves)
-      uint32_t S2, T3l, T3h, T4l, T4h;
-      if constexpr (FPM) {
-        const uint64_t b3 = (uint64_t)__double_as_longlong(wave_sum_f64(a3));
-        const uint64_t b4 = (uint64_t)__double_as_longlong(wave_sum_f64(a4));
-        S2 = 0;
-        T3l = (uint32_t)b3;
-        T3h = (uint32_t)(b3 >> 32);
-        T4l = (uint32_t)b4;
-        T4h = (uint32_t)(b4 >> 32);
-      } else {
-        S2 = wave_sum_u32(sd.s2);
-        T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
-        T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
-        T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
-        T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
+      if constexpr (FPM) {  // the fp64 d^3 / d^4 sums, parked as their two 32-bit halves
+        const uint64_t b3 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(a3, 153)));
+        const uint64_t b4 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(a4, 204)));
+        kT3l = mine ? (uint32_t)b3 : kT3l;
+        kT3h = mine ? (uint32_t)(b3 >> 32) : kT3h;
+        kT4l = mine ? (uint32_t)b4 : kT4l;
+        kT4h = mine ? (uint32_t)(b4 >> 32) : kT4h;
       }
-      const uint32_t P1 = (uint32_t)group_sum_i32<16>((int)sp.s1);
-      const uint32_t P2 = (uint32_t)group_sum_i32<16>((int)sp.s2);
-      const uint32_t P3 = (uint32_t)group_sum_i32<16>(sp.t3);
-      const uint32_t P4l = (uint32_t)group_sum_i32<16>((int)(sp.t4 & 0xFFFFFFu));
-      const uint32_t P4h = (uint32_t)group_sum_i32<16>((int)(sp.t4 >> 24));
-      // ---- park the row's totals in lane i (profile sums: lane 0's row-0 values)
-      const bool mine = lane == i;
-      kS1 = mine ? S1 : kS1;
-      kS2 = mine ? S2 : kS2;
-      kT3l = mine ? T3l : kT3l;
-      kT3h = mine ? T3h : kT3h;
-      kT4l = mine ? T4l : kT4l;
-      kT4h = mine ? T4h : kT4h;
-      kP1 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P1) : kP1;
-      kP2 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P2) : kP2;
-      kP3 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P3) : kP3;
-      kP4l = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4l) : kP4l;
-      kP4h = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4h) : kP4h;
       kssq = mine ? ssq : kssq;
     }
     // ---- finalise the batch: lane i -> row base + i
