@@ -119,6 +119,9 @@ int pfe_synchronize(pfe_handle* h);
  *                        1 = the round-3 kernels, 2 = as 0 with skew / kurt from fp64 d^3 / d^4
  *                        sums (A/B).  Mean and std are numpy's bits either way; skew / kurt
  *                        may differ in the last bits (scipy's m2 vs the exact one)
+ *   PFE_OPT_PFD_SPLIT    PFD preprocessing: 1 = the folds' part sums streamed by their own kernel
+ *                        on a side stream while the sweep kernel works on the previous chunk
+ *                        (default), 0 = one fused kernel (same bits)
  * Returns PFE_EINVAL for an unknown option or an out-of-range value.
  * --------------------------------------------------------------------------------------- */
 #define PFE_OPT_SOLVER 1
@@ -129,6 +132,7 @@ int pfe_synchronize(pfe_handle* h);
 #define PFE_OPT_LYON8_BURST 6
 #define PFE_OPT_PFD_WAVES 7
 #define PFE_OPT_LYON8_DM 8
+#define PFE_OPT_PFD_SPLIT 9
 #define PFE_SOLVER_POOLED 0
 #define PFE_SOLVER_BATCHED 1
 #define PFE_SOLVER_WAVE 2

@@ -57,6 +57,8 @@ struct pfe_handle {
   hipEvent_t ev_in[PIPE_SLOTS] = {}, ev_k[PIPE_SLOTS] = {}, ev_out[PIPE_SLOTS] = {};
   void* pin = nullptr;
   size_t pin_bytes = 0;
+  // split PFD pipeline (pfe_pfd_dmprof): two events per part-sum buffer, made on first use
+  hipEvent_t pev[4] = {};
   std::string err;
 };
 
@@ -195,6 +197,8 @@ void pfe_destroy(pfe_handle* h) {
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t& v : h->fork.ev)
     if (v) (void)hipEventDestroy(v);
+  for (hipEvent_t& v : h->pev)
+    if (v) (void)hipEventDestroy(v);
   for (int i = 0; i < PIPE_SLOTS; ++i) {
     if (h->ev_in[i]) (void)hipEventDestroy(h->ev_in[i]);
     if (h->ev_k[i]) (void)hipEventDestroy(h->ev_k[i]);
@@ -262,6 +266,10 @@ int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
       if (v < 0 || v > 2) break;
       o.lyon8_dm = (int)v;
       return PFE_OK;
+    case PFE_OPT_PFD_SPLIT:
+      if (v != 0 && v != 1) break;
+      o.pfd_split = (int)v;
+      return PFE_OK;
     default:
       return set_err(h, PFE_EINVAL, "pfe_set_option: unknown option %d", option);
   }
@@ -281,6 +289,7 @@ int pfe_get_option(const pfe_handle* h, int32_t option, int64_t* v) {
     case PFE_OPT_LYON8_BURST: *v = o.lyon8_burst; return PFE_OK;
     case PFE_OPT_PFD_WAVES: *v = o.pfd_waves; return PFE_OK;
     case PFE_OPT_LYON8_DM: *v = o.lyon8_dm; return PFE_OK;
+    case PFE_OPT_PFD_SPLIT: *v = o.pfd_split; return PFE_OK;
     default: return PFE_EINVAL;
   }
 }
@@ -621,7 +630,20 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
   a.n = n;
   a.waves = h->opt.pfd_waves;
   const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
+  // split pipeline: two buffers of part sums, chunks of up to 4096 folds (128 MB at 32 x 128)
+  const bool split = h->opt.pfd_split && h->fork.side[0] && pfe::pfd_split_ok(a);
+  const int64_t chunk = n < 4096 ? n : 4096;
+  const size_t wsb = split ? align256(2 * (size_t)chunk * in->nsub * in->proflen * sizeof(double)) : 0;
+  size_t wsoff = 0;
+  if (split) {
+    for (hipEvent_t& v : h->pev)
+      if (!v) PFE_HIP(h, hipEventCreateWithFlags(&v, hipEventDisableTiming));
+  }
   if (flags & PFE_FLAG_DEVICE_PTRS) {
+    if (split) {
+      rc = ensure_scratch(h, wsb);
+      if (rc) return rc;
+    }
     a.profs = in->profs;
     a.subfreqs = in->subfreqs;
     a.scal = in->scal;
@@ -637,8 +659,9 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
     const size_t xb = chis ? align256((size_t)n * PFE_PFD_NDM * sizeof(float)) : 0;
     const size_t lb = lyon8 ? align256((size_t)n * 8 * sizeof(double)) : 0;
     const size_t tb = align256((size_t)n * sizeof(uint32_t));
-    rc = ensure_scratch(h, pb + fb + cb + ob + xb + lb + tb);
+    rc = ensure_scratch(h, pb + fb + cb + ob + xb + lb + tb + wsb);
     if (rc) return rc;
+    wsoff = pb + fb + cb + ob + xb + lb + tb;
     char* base = (char*)h->scratch;
     size_t off = 0;
     PFE_HIP(h, hipMemcpyAsync(base, in->profs, np * sizeof(double), hipMemcpyHostToDevice, st));
@@ -660,7 +683,10 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
     off += lb;
     a.status = (uint32_t*)(base + off);
   }
-  hipError_t e = pfe::launch_pfd_dmprof(a, st);
+  hipError_t e = split ? pfe::launch_pfd_dmprof_split(a, st, h->fork.side[0],
+                                                      (double*)((char*)h->scratch + wsoff), chunk,
+                                                      h->pev)
+                       : pfe::launch_pfd_dmprof(a, st);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "pfd_dmprof launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     if (profile)

@@ -23,7 +23,18 @@ struct PfdArgs {
   double* out22 = nullptr;
   double* par22 = nullptr;
   int waves = 4;  // handle option PFE_OPT_PFD_WAVES: the four-wave kernel (<= 128 bins) or one wave
+  // the folds' part sums T (n x nsub x L, k_pfd_parts) read from global memory instead of
+  // reduced in the kernel (split pipeline), or null (fused)
+  const double* tin = nullptr;
 };
+
+// split pipeline of pfe_pfd_dmprof: k_pfd_parts streams chunks of `chunk` folds' part sums
+// into the two halves of ws (2 x chunk x nsub x L doubles) on `side` while k_pfd_dmprof4
+// sweeps the previous chunk on `st`; ev: four events (two per buffer).  False when the
+// shape takes the fused kernels (> 128 bins or the four-wave LDS limit).
+bool pfd_split_ok(const PfdArgs& a);
+hipError_t launch_pfd_dmprof_split(const PfdArgs& a, hipStream_t st, hipStream_t side, double* ws,
+                                   int64_t chunk, hipEvent_t (&ev)[4]);
 
 size_t pfd_lds_bytes(int nsub, int L);
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st);

@@ -909,8 +909,13 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   // T[j][b] = sum over parts of the rotated sub-integration profiles (profs.sum(0)): each
   // thread keeps PFD4_E elements and walks the parts, so PFD4_E loads are in flight per
   // thread and step; wave 3 first tabulates the sweep's rotations (below), overlapping them
-  // with its first loads
-  {
+  // with its first loads.  Split pipeline: T comes from k_pfd_parts (the same sums).
+  if (a.tin) {
+    const int total = NS * L;
+    const double* tg = a.tin + c * (int64_t)total;
+    if (wv == 3 && sweep) sweep_rotations(rot, sdb, fr, NS, L, bps, dm_lo, dm_hi, lane);
+    for (int e = tid; e < total; e += 256) T[e] = tg[e];
+  } else {
     const int total = NS * L;
     const int64_t pstride = (int64_t)NS * L;
     for (int e0 = tid; e0 < total; e0 += 256 * PFD4_E) {
@@ -1043,6 +1048,66 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
+// Split pipeline, stage 1: the fold's part sums T (as k_pfd_dmprof4 reduces them: the
+// dedispersion rotations of wave 0, then each element summing its parts in order) streamed
+// to global memory.  Little LDS and no sweep state, so many blocks per CU keep enough loads
+// in flight to stream the folds at HBM rate while k_pfd_dmprof4 sweeps the previous chunk.
+__global__ __launch_bounds__(256) void k_pfd_parts(PfdArgs a, double* __restrict__ tout) {
+  extern __shared__ double lds[];
+  const int64_t c = blockIdx.x;
+  if (c >= a.n) return;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int NP = a.npart, NS = a.nsub, L = a.L;
+  double* dl = lds;               // NS
+  int* cum = (int*)(dl + NS);     // NS
+  const double* sc = a.scal + c * PFE_PFD_NSCAL;
+  const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
+  const double* fr = a.subfreqs + c * NS;
+  const double* P = a.profs + c * (int64_t)NP * NS * L;
+  if ((tid >> 6) == 0) {  // PFDFile.py:346-373 (interp = 0), as k_pfd_dmprof4's wave 0
+    for (int j = lane; j < NS; j += 64) dl[j] = delay_from_dm(bestdm, fr[j]);
+    lds_sync();
+    const double hif = dl[NS - 1];
+    for (int j = lane; j < NS; j += 64) {
+      const double delaybins = (dl[j] - hif) * bps - 0.0;
+      const double nw = floor(delaybins + 0.5);
+      cum[j] = pymod((long long)nw, L);
+    }
+  }
+  __syncthreads();
+  const int total = NS * L;
+  const int64_t pstride = (int64_t)NS * L;
+  double* tg = tout + c * (int64_t)total;
+  for (int e0 = tid; e0 < total; e0 += 256 * PFD4_E) {
+    int src[PFD4_E];
+    bool ok[PFD4_E];
+    double acc[PFD4_E];
+#pragma unroll
+    for (int u = 0; u < PFD4_E; ++u) {
+      const int e = e0 + 256 * u;
+      ok[u] = e < total;
+      const int j = ok[u] ? e / L : 0;
+      const int b = ok[u] ? e - j * L : 0;
+      const int r = cum[j];
+      src[u] = j * L + (b + r < L ? b + r : b + r - L);
+      acc[u] = ok[u] ? __builtin_nontemporal_load(P + src[u]) : 0.0;
+    }
+#pragma unroll 2
+    for (int p = 1; p < NP; ++p) {
+      double v[PFD4_E];
+#pragma unroll
+      for (int u = 0; u < PFD4_E; ++u)
+        v[u] = ok[u] ? __builtin_nontemporal_load(P + p * pstride + src[u]) : 0.0;
+#pragma unroll
+      for (int u = 0; u < PFD4_E; ++u) acc[u] += v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PFD4_E; ++u)
+      if (ok[u]) tg[e0 + 256 * u] = acc[u];
+  }
+}
+
 size_t pfd_lds_bytes(int nsub, int L) {
   return ((size_t)nsub * L + 2 * (size_t)L + 3 * (size_t)nsub) * sizeof(double) +
          (size_t)nsub * sizeof(int) + 64;
@@ -1051,6 +1116,57 @@ size_t pfd_lds_bytes(int nsub, int L) {
 static size_t pfd4_lds_bytes(int nsub, int L) {
   return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int) + 8 +
          4 * 256 * sizeof(double);
+}
+
+bool pfd_split_ok(const PfdArgs& a) {
+  return a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4;
+}
+
+// the folds [c0, c0 + cn) of a batch: every per-fold pointer moved to fold c0
+static PfdArgs pfd_chunk(const PfdArgs& a, int64_t c0, int64_t cn) {
+  PfdArgs b = a;
+  b.n = cn;
+  b.profs = a.profs + c0 * (int64_t)a.npart * a.nsub * a.L;
+  b.subfreqs = a.subfreqs + c0 * a.nsub;
+  b.scal = a.scal + c0 * PFE_PFD_NSCAL;
+  if (a.profile) b.profile = a.profile + c0 * a.L;
+  if (a.chis) b.chis = a.chis + c0 * PFE_PFD_NDM;
+  if (a.lyon8) b.lyon8 = a.lyon8 + c0 * 8;
+  if (a.status) b.status = a.status + c0;
+  if (a.out22) b.out22 = a.out22 + c0 * 22;
+  if (a.par22) b.par22 = a.par22 + c0 * 8;
+  return b;
+}
+
+hipError_t launch_pfd_dmprof_split(const PfdArgs& a, hipStream_t st, hipStream_t side, double* ws,
+                                   int64_t chunk, hipEvent_t (&ev)[4]) {
+  const size_t lds4 = pfd4_lds_bytes(a.nsub, a.L);
+  hipError_t e = ensure_dyn_lds<k_pfd_dmprof4>(lds4);
+  if (e != hipSuccess) return e;
+  const size_t ldsp = (size_t)a.nsub * (sizeof(double) + sizeof(int)) + 16;
+  const int64_t per = (int64_t)a.nsub * a.L;
+  // side waits for everything queued on st before the call (the inputs may come from it)
+  if ((e = hipEventRecord(ev[2], st)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(side, ev[2], 0)) != hipSuccess) return e;
+  int k = 0;
+  for (int64_t c0 = 0; c0 < a.n; c0 += chunk, ++k) {
+    const int64_t cn = a.n - c0 < chunk ? a.n - c0 : chunk;
+    const int buf = k & 1;
+    double* t = ws + (size_t)buf * chunk * per;
+    const PfdArgs b = pfd_chunk(a, c0, cn);
+    // buffer reuse: chunk k - 2's sweep (on st) has read this half
+    if (k >= 2 && (e = hipStreamWaitEvent(side, ev[2 + buf], 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pfd_parts, dim3((unsigned)cn), dim3(256), ldsp, side, b, t);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev[buf], side)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, ev[buf], 0)) != hipSuccess) return e;
+    PfdArgs d = b;
+    d.tin = t;
+    hipLaunchKernelGGL(k_pfd_dmprof4, dim3((unsigned)cn), dim3(256), lds4, st, d);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev[2 + buf], st)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {

@@ -15,7 +15,7 @@ Bar:
 import numpy as np
 import pytest
 
-from golden_util import SELF_NOISY, bates_inputs, load
+from golden_util import SELF_NOISY, bates_inputs, envelope_check, load
 from oracle.bates import bates22
 from oracle.lyon import lyon8
 
@@ -49,10 +49,19 @@ def test_bates22_oracle_vs_reference(name, rows):
     with np.errstate(all="ignore"):
         close = same | (np.abs(got - ref) <= 1e-5 * np.abs(ref))
     for j in range(22):
-        if j in SELF_NOISY:
-            assert close[:, j].mean() >= 0.70, f"s{j + 1}: {close[:, j].mean():.3f}"
-        else:
+        if j not in SELF_NOISY:
             assert same[:, j].all(), f"s{j + 1} not bit-exact in {(~same[:, j]).sum()} rows"
+    # s10/s11: the rows inside the reference's envelope (tight rows all, chaotic rows to the
+    # binomial bound); the 70% single-draw agreement only where no envelope row decides
+    full = np.full(d["out"].shape, np.nan)
+    full[sel] = out
+    fst = np.ones(len(ok), dtype=np.int64)
+    fst[sel] = st
+    stats = envelope_check(full, fst, name, skip=[j for j in range(22) if j not in SELF_NOISY])
+    for j in SELF_NOISY:
+        tight_rows, wide_rows = stats[j + 1][0], stats[j + 1][1]
+        if tight_rows + wide_rows == 0:
+            assert close[:, j].mean() >= 0.70, f"s{j + 1}: {close[:, j].mean():.3f}"
 
 
 def test_bates22_oracle_vs_reference_nsub32():

@@ -86,3 +86,28 @@ def test_fresh_shapes_vs_oracle(engine, tmp_path):
                 got = r["lyon8"][i]
                 for j in (0, 1, 3, 4, 5, 7):
                     assert eq_nan(got[j], ref[j]), (L, i, j, got[j], ref[j])
+
+
+def test_split_pipeline_bit_identical(engine, tmp_path):
+    """PFE_OPT_PFD_SPLIT: the part sums streamed by k_pfd_parts on the side stream (three
+    chunks of 4096 folds, both buffers reused) give the fused kernel's bits."""
+    from pulsarfeatureextractor_amd.synth import pfd_candidate
+
+    files = []
+    for i in range(4):
+        c = pfd_candidate(np.random.default_rng(900 + i), 4, 16, 128)
+        p = os.path.join(tmp_path, f"s{i}.pfd")
+        pfd.write(p, **c)
+        files.append(p)
+    profs, subfreqs, scal = pfd.batch_inputs([pfd.read(f) for f in files])
+    n = 9000
+    rng = np.random.default_rng(7)
+    idx = np.arange(n) % 4
+    profs = profs[idx] + rng.standard_normal((n,) + profs.shape[1:])
+    subfreqs, scal = subfreqs[idx].copy(), scal[idx].copy()
+    out = {}
+    for split in (0, 1):
+        with engine.options(pfd_split=split):
+            out[split] = engine.pfd_dmprof(profs, subfreqs, scal)
+    for k in ("profile", "chis", "lyon8", "status"):
+        assert eq_nan(out[0][k], out[1][k]).all(), k
