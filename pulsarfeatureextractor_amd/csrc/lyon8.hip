@@ -729,6 +729,7 @@ __global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ 
 //     rows) and parked in lane (row mod 64); the 8 statistics of a batch of <= 64 rows are
 //     finalised once, one row per lane, and stored as one 4 KiB span -- the divisions,
 //     square roots and 128-bit numerators run once per 64 rows instead of once per row;
+//   * the profile row (64-256 bytes) is summed there too, by the lane that finalises it;
 //   * each wave owns a contiguous range of rows (no grid-stride tail imbalance).
 // Row layout (numpy's reduction of nDM x 128 values): NCH chunks of 8192, the first NCH-1
 // full (64 leaves of 128), the last one numpy's pairwise tree of <= 64 leaves of 64..128
@@ -883,8 +884,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   // buffer descriptors)
   const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t r0 = n * wave / nwaves, r1 = n * (wave + 1) / nwaves;
-  const int ppl = sh.lp >> 4;                            // lanes holding the profile
-  const int pl = lane < ppl ? lane : 0;
+  const int ppl = sh.lp >> 4;  // 16-byte pieces of the profile
   int zpad = 0;  // zero bytes this lane reads past the row
 #pragma unroll
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
@@ -903,7 +903,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   for (int64_t base = r0; base < r1; base += 64) {
     const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
     uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
-    uint32_t kP1 = 0, kP2 = 0, kP3 = 0, kP4l = 0, kP4h = 0;
     double kssq = 0.0;
     for (int i = 0; i < cnt; ++i) {
       const int64_t c = base + i;
@@ -911,7 +910,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       // ld bytes, so pieces past the row read as zero bytes (corrected below)
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<uint8_t*>(dm + c * ds), 0, sh.ld, 0x00020000);
-      const u32x4 pq = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(prof + c * ps) + pl);
       u32x4 q[NPMAX];
 #pragma unroll
       for (int k = 0; k < NPMAX; ++k)
@@ -933,9 +931,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         sd.t3 += zpad << 21;
         sd.t4 -= (uint64_t)zpad << 28;
       }
-      Acc2 sp = {0, 0, 0, 0};  // (every lane, no branch: a branch here drains vmcnt)
-      acc2_x4(pq, sp);
-      if (lane >= ppl) sp = (Acc2){0, 0, 0, 0};
       // ---- numpy's sum of squared deviations, chunk by chunk through the LDS image
       // (chunk 0 is staged before the mean is known, so its registers die early)
       dm_stage<NCH>(img, q, 0, lane, full_base, stab);
@@ -943,8 +938,9 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       const double mean = (double)S1 / (double)sh.ld;
       const double nm = -__builtin_ldexp(mean, -51);  // exact
       // ---- the integer row totals (exact 32-bit halves) are reduced and parked in lane i
-      // now, so their registers are free during the byte loop; profile sums: row 0's
+      // now, so their registers are free during the byte loop
       const bool mine = lane == i;
+      kS1 = mine ? S1 : kS1;
       if constexpr (!FPM) {
         const uint32_t S2 = wave_sum_u32(sd.s2);
         const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
@@ -956,19 +952,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         kT3h = mine ? T3h : kT3h;
         kT4l = mine ? T4l : kT4l;
         kT4h = mine ? T4h : kT4h;
-      }
-      {
-        const uint32_t P1 = (uint32_t)group_sum_i32<16>((int)sp.s1);
-        const uint32_t P2 = (uint32_t)group_sum_i32<16>((int)sp.s2);
-        const uint32_t P3 = (uint32_t)group_sum_i32<16>(sp.t3);
-        const uint32_t P4l = (uint32_t)group_sum_i32<16>((int)(sp.t4 & 0xFFFFFFu));
-        const uint32_t P4h = (uint32_t)group_sum_i32<16>((int)(sp.t4 >> 24));
-        kS1 = mine ? S1 : kS1;
-        kP1 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P1) : kP1;
-        kP2 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P2) : kP2;
-        kP3 = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P3) : kP3;
-        kP4l = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4l) : kP4l;
-        kP4h = mine ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P4h) : kP4h;
       }
       double ssq = 0.0, a3 = 0.0, a4 = 0.0;
 #pragma unroll
@@ -1002,13 +985,17 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
     }
     // ---- finalise the batch: lane i -> row base + i
     if (lane < cnt) {
-      // profile (lp a power of two: every moment is the correctly rounded exact rational)
+      // profile: lane i sums row base + i's lp bytes itself (exact power sums, once per 64
+      // rows; lp a power of two: every moment is the correctly rounded exact rational)
+      Acc2 sp = {0, 0, 0, 0};
+      const u32x4* pr = reinterpret_cast<const u32x4*>(prof + (base + lane) * ps);
+      for (int k = 0; k < ppl; ++k) acc2_x4(__builtin_nontemporal_load(pr + k), sp);
       const long long L = sh.lp;
-      const long long S1p = (long long)kP1;
+      const long long S1p = (long long)sp.s1;
       const long long T1p = S1p - 128ll * L;
-      const long long T2p = (long long)kP2 - 256ll * S1p + 16384ll * L;
-      const long long T3p = (long long)(int)kP3;
-      const uint64_t T4p = ((uint64_t)kP4h << 24) + (uint64_t)kP4l;
+      const long long T2p = (long long)sp.s2 - 256ll * S1p + 16384ll * L;
+      const long long T3p = (long long)sp.t3;
+      const uint64_t T4p = sp.t4;
       const Moments mp = moments_i64(L, T1p, T2p, T3p, T4p);
       const double sdp = sqrt(mp.m2);
       const bool zp = zero_var(mp);

@@ -87,7 +87,7 @@ def lyon_batch_torch(n: int, lp: int = 128, ld: int = 128, seed: int = BASE_SEED
 
     def rows(L):
         out = torch.empty((n, L), dtype=torch.uint8, device=device)
-        chunk = 1 << 20
+        chunk = 1 << 20 if L <= 1024 else max(1, (1 << 28) // L)  # float temporaries <= 1 GiB
         t = torch.arange(L, device=device, dtype=torch.float32)[None, :]
         for s in range(0, n, chunk):
             m = min(chunk, n - s)

@@ -6,7 +6,7 @@ import numpy as np
 
 sys.path.insert(0, ".")
 from oracle.lyon import lyon8_batched  # noqa: E402
-from pulsarfeatureextractor_amd import Engine  # noqa: E402
+from pulsarfeatureextractor_amd._native import Engine  # noqa: E402
 from pulsarfeatureextractor_amd.synth import lyon_batch  # noqa: E402
 
 

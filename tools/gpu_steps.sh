@@ -16,7 +16,9 @@
 #   l8long       tools/lyon8_long_bench.py over DataBlock lengths (LDS=... ops via L8OPT)
 #   trace_l8dm   kernel trace of the nDM = 120 Lyon-8 kernel (tools/lyon8_long_bench.py)
 #   pmc_l8dm     FETCH_SIZE / WRITE_SIZE passes of the nDM = 120 command
+#   sq_l8dm      two SQ counter passes over the nDM = 120 kernel + tools/sq_summary.py
 #   e2e          tools/e2e_bench.py --mode stream on 50 000 synthetic PHCX files
+#   pfdab        bench.py --path pfd with the split pipeline (default) and fused (pfd_split=0)
 #   pytest:<f>   one test file, e.g. pytest:tests/test_lyon8_gpu.py
 set -o pipefail
 export TMPDIR=/tmp
@@ -78,9 +80,26 @@ for step in "$@"; do
           python3 tools/lyon8_long_bench.py --n 1000000 --ld 15360 --steps 5 > $O/${T}_pmc_l8dm_$c.log 2>&1 \
           || fail pmc_l8dm $O/${T}_pmc_l8dm_$c.log
       done ;;
+    sq_l8dm)
+      P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY"
+      P2="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT"
+      i=0
+      for p in "$P1" "$P2"; do
+        i=$((i + 1))
+        timeout -s KILL 180 rocprofv3 --pmc $p --output-format csv -d $O/${T}_sql8dm/p$i -o pmc -- \
+          python3 tools/lyon8_long_bench.py --n 1000000 --ld ${L8LD:-15360} --steps 2 ${L8OPT} \
+          > $O/${T}_sql8dm_p$i.log 2>&1 || fail sq_l8dm $O/${T}_sql8dm_p$i.log
+      done
+      python3 tools/sq_summary.py $O/${T}_sql8dm/p1 $O/${T}_sql8dm/p2 > $O/${T}_sql8dm_summary.json ;;
     e2e)
       timeout -k 10 600 python -u tools/e2e_bench.py --mode stream --n 50000 --dir /tmp/pfe_e2e \
         --depth ${E2E_DEPTH:-1,2} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;
+    pfdab)
+      for v in 1 0; do
+        timeout -k 10 300 python3 bench.py --path pfd --steps 10 --warmup 2 --no-cpu-baseline \
+          --option pfd_split=$v > $O/${T}_pfd_split$v.json 2> $O/${T}_pfd_split$v.err \
+          || fail pfdab $O/${T}_pfd_split$v.err
+      done ;;
     pytest:*)
       f=${step#pytest:}
       n=$(basename "$f" .py)
