@@ -73,8 +73,8 @@ OPTIONS = {
     "lyon8_blocks": 5,
     "lyon8_burst": 6,
     "pfd_waves": 7,
-    "lyon8_dm": 8,      # 0 per-byte DataBlock kernel (default), 1 the round-3 kernels, 2 A/B
-    "pfd_split": 9,     # 1 part sums streamed beside the sweep (default), 0 fused kernel
+    "lyon8_dm": 8,      # 0 DataBlock teams kernel (default), 1 round 3, 2 fp64 moments, 3 one wave
+    "pfd_split": 9,     # 0 fused kernel (default), 1 part sums streamed beside the sweep
 }
 SOLVERS = {"pooled": 0, "batched": 1, "wave": 2}
 

@@ -16,8 +16,8 @@ struct Options {
   int lyon8_blocks = 16384;        // grid cap of the Lyon-8 stream kernel
   int lyon8_burst = 2;             // candidate groups per wave step of the Lyon-8 kernel
   int pfd_waves = 4;               // waves per fold of the PFD dmprof kernel (4 or 1)
-  int lyon8_dm = 0;                // DataBlock DM rows: 0 lyon8_u8_dm, 1 the round-3 kernels
-  int pfd_split = 1;               // PFD dmprof: 1 part sums streamed by k_pfd_parts beside the sweep, 0 fused
+  int lyon8_dm = 0;                // DataBlock DM rows: 0 lyon8_u8_dmt, 1 round 3, 2 FPM, 3 lyon8_u8_dm
+  int pfd_split = 0;               // PFD dmprof: 1 part sums by k_pfd_parts beside the sweep, 0 fused
 };
 
 }  // namespace pfe
