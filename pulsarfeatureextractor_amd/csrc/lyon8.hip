@@ -853,15 +853,112 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
   }
 }
 
+// dm_leaf with its phases pinned apart: a word's eight conversions, the next word's LDS
+// reads, then the squares and chain adds (see lyon8_u8_dmt below)
+template <bool FPM, bool PARTIAL>
+__device__ __forceinline__ double dm_leaf_p(const uint8_t* lb, double nm, double sc,
+                                            const uint32_t (&z)[8], int nw, double& a3, double& a4) {
+  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
+  lds_u8* vb = (lds_u8*)lb;
+  double r[8];
+  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
+  uint32_t x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = vb[j];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    // phases kept apart by scheduling barriers: the word's eight conversions, the next word's
+    // reads (into the same registers), then the squares and the ordered chain adds -- the
+    // reads' latency runs under 16 fp64 operations and the eight chains stay independent
+    double d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      d[j] = __builtin_fma(sc, __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]), nm);
+    // (the empty asm statements order the phases in the IR, the scheduling barriers in the
+    // machine code: without them every read of the leaf is hoisted, one VGPR each)
+    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
+                 "+v"(d[6]), "+v"(d[7]));
+    __builtin_amdgcn_sched_barrier(0);
+    if (k < 15) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = vb[8 * (k + 1) + j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
+                 "+v"(d[6]), "+v"(d[7]));
+    if (!PARTIAL || k < 8 || k < nw) {
+      double sq[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq[j] = d[j] * d[j];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        r[j] = k == 0 ? sq[j] : r[j] + sq[j];
+        if constexpr (FPM) {
+          c3[j & 1] = __builtin_fma(sq[j], d[j], c3[j & 1]);
+          c4[j & 1] = __builtin_fma(sq[j], sq[j], c4[j & 1]);
+        }
+      }
+    }
+    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]));
+    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  a3 = c3[0] + c3[1];
+  a4 = c4[0] + c4[1];
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+// numpy's 8 leaf chains over the words k < nw of the leaf at lb, each byte's rounded square
+// read from the row's table tab (256 doubles in LDS): a ds_read_u8 of the byte, its table
+// read, and the ordered add; the next word's byte reads are issued before this word's adds
+template <bool PARTIAL>
+__device__ __forceinline__ double dm_leaf_tab(const uint8_t* lb, const double* tab, int nw) {
+  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
+  typedef const __attribute__((address_space(3))) double lds_f64;
+  lds_u8* vb = (lds_u8*)lb;
+  lds_f64* tb = (lds_f64*)tab;
+  double r[8];
+  uint32_t x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = vb[j];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    double t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = tb[x[j]];
+    if (k < 15) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = vb[8 * (k + 1) + j];
+    }
+    if (!PARTIAL || k < 8 || k < nw) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = k == 0 ? t[j] : r[j] + t[j];
+    }
+    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]));
+  }
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
 // FPM (PFE_OPT_LYON8_DM = 2, A/B): skew / kurt from fp64 d^3 / d^4 sums fused into the byte
 // loop (2 FMAs per byte) instead of the exact integer power sums (3 packed ops per byte)
-template <int NCH, bool FPM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : 2, NCH <= 2 ? 4 : 2)))
+// TAB: the row's 256 rounded squares fl(fl(v - mean)^2) tabulated in LDS once the mean is
+// known; each byte then costs a table read and the ordered add (dm_leaf_tab), not the
+// conversion, square and add (3 blocks of 4 waves per CU: 43 KB of LDS per block)
+#ifndef PFE_DM_WPE
+#define PFE_DM_WPE 4
+#endif
+template <int NCH, bool FPM, bool TAB = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAB ? 3 : NCH <= 2 ? PFE_DM_WPE : 2, TAB ? 3 : NCH <= 2 ? PFE_DM_WPE : 2)))
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
+  static_assert(!(TAB && FPM), "the table variant keeps the exact power sums");
   constexpr int NPMAX = 8 * NCH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
+  __shared__ double tabs[TAB ? 4 : 1][TAB ? 256 : 1];
   __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
   const int lane = threadIdx.x & 63;
   uint8_t* img = lds[threadIdx.x >> 6];
@@ -937,6 +1034,15 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
       const double nm = -__builtin_ldexp(mean, -51);  // exact
+      if constexpr (TAB) {  // numpy's fl(fl(v - mean)^2) for every byte value v
+        typedef __attribute__((address_space(3))) double lds_f64;
+        lds_f64* tb = (lds_f64*)tabs[threadIdx.x >> 6];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double d = (double)(lane + 64 * u) - mean;
+          tb[lane + 64 * u] = d * d;
+        }
+      }
       // ---- the integer row totals (exact 32-bit halves) are reduced and parked in lane i
       // now, so their registers are free during the byte loop
       const bool mine = lane == i;
@@ -959,7 +1065,19 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
         double l3, l4;
-        double leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
+        double leaf;
+        if constexpr (TAB) {
+          l3 = l4 = 0.0;
+          leaf = ch < NCH - 1 ? dm_leaf_tab<false>(img + lane * DM_S, tabs[threadIdx.x >> 6], 16)
+                              : dm_leaf_tab<true>(img + lane * DM_S, tabs[threadIdx.x >> 6], nw_last);
+        } else {
+#if defined(PFE_DM_LEAFP) && PFE_DM_LEAFP
+          leaf = ch < NCH - 1 ? dm_leaf_p<FPM, false>(img + lane * DM_S, nm, sc, z, 16, l3, l4)
+                              : dm_leaf_p<FPM, true>(img + lane * DM_S, nm, sc, z, nw_last, l3, l4);
+#else
+          leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
+#endif
+        }
         if (ch == NCH - 1) {
           const bool in = lane < sh.leaves_last;
           leaf = in ? leaf : 0.0;
@@ -1048,61 +1166,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
 //     next word's LDS reads between a word's fma and its mul / add, so the reads' latency and
 //     the fp64 dependencies overlap.
 // NCH = 1 (rows <= 8192 bytes): four one-wave teams per block.
-template <bool FPM, bool PARTIAL>
-__device__ __forceinline__ double dm_leaf_p(const uint8_t* lb, double nm, double sc,
-                                            const uint32_t (&z)[8], int nw, double& a3, double& a4) {
-  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
-  lds_u8* vb = (lds_u8*)lb;
-  double r[8];
-  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
-  uint32_t x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = vb[j];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    // phases kept apart by scheduling barriers: the word's eight conversions, the next word's
-    // reads (into the same registers), then the squares and the ordered chain adds -- the
-    // reads' latency runs under 16 fp64 operations and the eight chains stay independent
-    double d[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      d[j] = __builtin_fma(sc, __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]), nm);
-    // (the empty asm statements order the phases in the IR, the scheduling barriers in the
-    // machine code: without them every read of the leaf is hoisted, one VGPR each)
-    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
-                 "+v"(d[6]), "+v"(d[7]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (k < 15) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = vb[8 * (k + 1) + j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
-                 "+v"(d[6]), "+v"(d[7]));
-    if (!PARTIAL || k < 8 || k < nw) {
-      double sq[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sq[j] = d[j] * d[j];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        r[j] = k == 0 ? sq[j] : r[j] + sq[j];
-        if constexpr (FPM) {
-          c3[j & 1] = __builtin_fma(sq[j], d[j], c3[j & 1]);
-          c4[j & 1] = __builtin_fma(sq[j], sq[j], c4[j & 1]);
-        }
-      }
-    }
-    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
-                 "+v"(r[6]), "+v"(r[7]));
-    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  a3 = c3[0] + c3[1];
-  a4 = c4[0] + c4[1];
-  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-}
-
 // stage one chunk (the wave's 8 pieces) into its LDS image: full chunks at leaf lane/8 + 8j,
 // the row's last chunk where the block's table says (0xFFFF: past the chunk)
 __device__ __forceinline__ void dm_stage1(uint8_t* img, const u32x4 (&q)[8], int lane, bool last,
@@ -1536,10 +1599,10 @@ static int resident_blocks() {
   return cached[dev];
 }
 
-template <int NCH, bool FPM>
+template <int NCH, bool FPM, bool TAB = false>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dm<NCH, FPM>;
+  constexpr auto K = lyon8_u8_dm<NCH, FPM, TAB>;
   int64_t blocks = resident_blocks<K>();
   const int64_t need = (n + 3) / 4;  // at least one row per wave
   if (blocks > need) blocks = need;
@@ -1574,6 +1637,13 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dmt (teams
     // of waves; option 2: its fp64-moment variant), option 3: the one-wave lyon8_u8_dm
     const int cap = o.lyon8_blocks;
+    if (o.lyon8_dm == 5 && dnch <= 2) {  // one wave per row, tabulated squares
+      if (dnch == 1)
+        launch_dm_kernel<1, false, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
+      else
+        launch_dm_kernel<2, false, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
+      return hipGetLastError();
+    }
     if (o.lyon8_dm == 4 && dnch <= 2) {  // one wave per row, fp64 d^3 / d^4 moments
       if (dnch == 1)
         launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap);

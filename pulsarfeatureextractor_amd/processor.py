@@ -230,6 +230,22 @@ def score_lyon8(cands, engine=None):
     return out
 
 
+def _cuts(n, batch):
+    """Batch boundaries of a streamed run: full batches, except that a long run starts and
+    ends with batch/8, batch/4, batch/2 so the GPU stage starts after a short first parse and
+    the last batch's scoring and output trail the last parse by little."""
+    ramp = [batch // 8, batch // 4, batch // 2]
+    if batch < 64 or n < 2 * sum(ramp) + batch:
+        return list(range(0, n, batch)) + [n]
+    sizes = list(ramp)
+    rem = n - 2 * sum(ramp)
+    while rem > 0:
+        sizes.append(min(batch, rem))
+        rem -= sizes[-1]
+    sizes += ramp[::-1]
+    return [0] + np.cumsum(sizes).tolist()
+
+
 def _stream(paths, parse, score, emit, batch=BATCH, depth=1):
     """parse(batch paths) on a helper thread, ahead of the GPU stage; score(parsed, slot) of
     batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
@@ -238,7 +254,7 @@ def _stream(paths, parse, score, emit, batch=BATCH, depth=1):
     scoring."""
     if not paths:
         return
-    cuts = list(range(0, len(paths), batch)) + [len(paths)]
+    cuts = _cuts(len(paths), batch)
     nb = len(cuts) - 1
 
     def part(k):

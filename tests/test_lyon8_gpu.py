@@ -122,7 +122,7 @@ def test_long_dm_rows_multibatch(engine, ld):
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
-@pytest.mark.parametrize("opt", [1, 2, 3])
+@pytest.mark.parametrize("opt", [1, 2, 3, 4, 5])
 def test_long_dm_rows_kernel_options_agree(engine, opt):
     """The round-3 DataBlock kernels (PFE_OPT_LYON8_DM = 1) and the fp64-moment A/B variant
     of lyon8_u8_dm (= 2) against the default: the same mean/std bits; skew/kurt agree to

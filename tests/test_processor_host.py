@@ -220,3 +220,17 @@ def test_default_workers_respects_omp(monkeypatch):
     assert processor.default_workers() <= 3
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert processor.default_workers() >= 1
+
+
+def test_stream_cuts_ramp():
+    """Long streamed runs ramp the batch size at both ends; every file is in exactly one
+    batch, in order; short runs keep plain batches."""
+    from pulsarfeatureextractor_amd.processor import _cuts
+
+    c = _cuts(50000, 8192)
+    sizes = np.diff(c)
+    assert c[0] == 0 and c[-1] == 50000 and (sizes > 0).all()
+    assert sizes[:3].tolist() == [1024, 2048, 4096] and sizes[-3:].tolist() == [4096, 2048, 1024]
+    assert sizes.max() == 8192
+    assert _cuts(100, 8192) == [0, 100]
+    assert _cuts(20, 8) == [0, 8, 16, 20]
