@@ -73,7 +73,7 @@ OPTIONS = {
     "lyon8_blocks": 5,
     "lyon8_burst": 6,
     "pfd_waves": 7,
-    "lyon8_dm": 8,      # 0 DataBlock teams kernel (default), 1 round 3, 2 fp64 moments, 3 one wave
+    "lyon8_dm": 8,      # DataBlock kernels: 0 default, 1 round 3, 2 exact power sums (pfe.h)
     "pfd_split": 9,     # 0 fused kernel (default), 1 part sums streamed beside the sweep
 }
 SOLVERS = {"pooled": 0, "batched": 1, "wave": 2}

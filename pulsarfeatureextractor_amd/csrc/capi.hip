@@ -263,7 +263,7 @@ int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
       o.pfd_waves = (int)v;
       return PFE_OK;
     case PFE_OPT_LYON8_DM:
-      if (v < 0 || v > 5) break;
+      if (v < 0 || v > 2) break;
       o.lyon8_dm = (int)v;
       return PFE_OK;
     case PFE_OPT_PFD_SPLIT:

@@ -716,13 +716,13 @@ __global__ __launch_bounds__(256) void lyon8_u8_lds(const uint8_t* __restrict__ 
   }
 }
 
-// ---- DataBlock rows, round 4: per-byte numpy chains at 4 VALU per byte ------------------
+// ---- DataBlock rows, round 4: per-byte numpy chains at 3 fp64 operations per byte --------
 // lyon8_u8_lds spent ~3.1 k VALU wave-instructions per 15 360-byte row (VALU-bound at 37 %
 // of HBM): byte extraction from 64-bit words, per-row 128-bit finalisation in every lane,
 // 64-bit wave reductions.  This kernel keeps numpy's arithmetic and removes the rest:
 //   * each byte of a leaf is read from the wave's padded LDS image with ds_read_u8 (the LDS
-//     unit zero-extends it: no VALU extraction), then cvt / sub / mul / add -- numpy's
-//     fl(fl(x - mean)^2) added to the leaf's running sum j = i mod 8 in order;
+//     unit zero-extends it: no VALU extraction), then one fma, one mul, one add (dm_leaf) --
+//     numpy's fl(fl(x - mean)^2) added to the leaf's running sum j = i mod 8 in order;
 //   * the exact power sums (mean, skew, kurt) come from the coalesced registers the row was
 //     loaded into, as the other Lyon-8 kernels compute them (v_dot4 / v_dot2);
 //   * the per-row totals are reduced as 32-bit halves (DPP in-row, permlane swaps across
@@ -853,112 +853,19 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
   }
 }
 
-// dm_leaf with its phases pinned apart: a word's eight conversions, the next word's LDS
-// reads, then the squares and chain adds (see lyon8_u8_dmt below)
-template <bool FPM, bool PARTIAL>
-__device__ __forceinline__ double dm_leaf_p(const uint8_t* lb, double nm, double sc,
-                                            const uint32_t (&z)[8], int nw, double& a3, double& a4) {
-  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
-  lds_u8* vb = (lds_u8*)lb;
-  double r[8];
-  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
-  uint32_t x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = vb[j];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    // phases kept apart by scheduling barriers: the word's eight conversions, the next word's
-    // reads (into the same registers), then the squares and the ordered chain adds -- the
-    // reads' latency runs under 16 fp64 operations and the eight chains stay independent
-    double d[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      d[j] = __builtin_fma(sc, __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]), nm);
-    // (the empty asm statements order the phases in the IR, the scheduling barriers in the
-    // machine code: without them every read of the leaf is hoisted, one VGPR each)
-    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
-                 "+v"(d[6]), "+v"(d[7]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (k < 15) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = vb[8 * (k + 1) + j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),
-                 "+v"(d[6]), "+v"(d[7]));
-    if (!PARTIAL || k < 8 || k < nw) {
-      double sq[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sq[j] = d[j] * d[j];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        r[j] = k == 0 ? sq[j] : r[j] + sq[j];
-        if constexpr (FPM) {
-          c3[j & 1] = __builtin_fma(sq[j], d[j], c3[j & 1]);
-          c4[j & 1] = __builtin_fma(sq[j], sq[j], c4[j & 1]);
-        }
-      }
-    }
-    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
-                 "+v"(r[6]), "+v"(r[7]));
-    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  a3 = c3[0] + c3[1];
-  a4 = c4[0] + c4[1];
-  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-}
-
-// numpy's 8 leaf chains over the words k < nw of the leaf at lb, each byte's rounded square
-// read from the row's table tab (256 doubles in LDS): a ds_read_u8 of the byte, its table
-// read, and the ordered add; the next word's byte reads are issued before this word's adds
-template <bool PARTIAL>
-__device__ __forceinline__ double dm_leaf_tab(const uint8_t* lb, const double* tab, int nw) {
-  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
-  typedef const __attribute__((address_space(3))) double lds_f64;
-  lds_u8* vb = (lds_u8*)lb;
-  lds_f64* tb = (lds_f64*)tab;
-  double r[8];
-  uint32_t x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = vb[j];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    double t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = tb[x[j]];
-    if (k < 15) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = vb[8 * (k + 1) + j];
-    }
-    if (!PARTIAL || k < 8 || k < nw) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = k == 0 ? t[j] : r[j] + t[j];
-    }
-    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
-                 "+v"(r[6]), "+v"(r[7]));
-  }
-  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-}
-
-// FPM (PFE_OPT_LYON8_DM = 2, A/B): skew / kurt from fp64 d^3 / d^4 sums fused into the byte
-// loop (2 FMAs per byte) instead of the exact integer power sums (3 packed ops per byte)
-// TAB: the row's 256 rounded squares fl(fl(v - mean)^2) tabulated in LDS once the mean is
-// known; each byte then costs a table read and the ordered add (dm_leaf_tab), not the
-// conversion, square and add (3 blocks of 4 waves per CU: 43 KB of LDS per block)
-#ifndef PFE_DM_WPE
-#define PFE_DM_WPE 4
-#endif
-template <int NCH, bool FPM, bool TAB = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAB ? 3 : NCH <= 2 ? PFE_DM_WPE : 2, TAB ? 3 : NCH <= 2 ? PFE_DM_WPE : 2)))
+// FPM (the default up to two chunks): skew / kurt from fp64 d^3 / d^4 sums fused into the
+// byte loop (2 fp64 FMAs per byte) instead of the exact integer power sums (3 packed integer
+// ops per byte).  Both run at half the VALU rate on gfx950 (profiles/r04_ubench_op_rates.txt:
+// ~5.1 and ~4.4 cycles per wave-instruction per SIMD), and the fp64 form frees the registers
+// of the 16-bit unpacking: 4.20 vs 4.47 ms per 1M rows at nDM = 120.  Beyond two chunks the
+// FPM form is not instantiated (the exact form needs no extra registers there).
+template <int NCH, bool FPM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : 2, NCH <= 2 ? 4 : 2)))
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
-  static_assert(!(TAB && FPM), "the table variant keeps the exact power sums");
   constexpr int NPMAX = 8 * NCH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
-  __shared__ double tabs[TAB ? 4 : 1][TAB ? 256 : 1];
   __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
   const int lane = threadIdx.x & 63;
   uint8_t* img = lds[threadIdx.x >> 6];
@@ -1034,15 +941,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       const uint32_t S1 = wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
       const double nm = -__builtin_ldexp(mean, -51);  // exact
-      if constexpr (TAB) {  // numpy's fl(fl(v - mean)^2) for every byte value v
-        typedef __attribute__((address_space(3))) double lds_f64;
-        lds_f64* tb = (lds_f64*)tabs[threadIdx.x >> 6];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const double d = (double)(lane + 64 * u) - mean;
-          tb[lane + 64 * u] = d * d;
-        }
-      }
       // ---- the integer row totals (exact 32-bit halves) are reduced and parked in lane i
       // now, so their registers are free during the byte loop
       const bool mine = lane == i;
@@ -1065,19 +963,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
         double l3, l4;
-        double leaf;
-        if constexpr (TAB) {
-          l3 = l4 = 0.0;
-          leaf = ch < NCH - 1 ? dm_leaf_tab<false>(img + lane * DM_S, tabs[threadIdx.x >> 6], 16)
-                              : dm_leaf_tab<true>(img + lane * DM_S, tabs[threadIdx.x >> 6], nw_last);
-        } else {
-#if defined(PFE_DM_LEAFP) && PFE_DM_LEAFP
-          leaf = ch < NCH - 1 ? dm_leaf_p<FPM, false>(img + lane * DM_S, nm, sc, z, 16, l3, l4)
-                              : dm_leaf_p<FPM, true>(img + lane * DM_S, nm, sc, z, nw_last, l3, l4);
-#else
-          leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
-#endif
-        }
+        double leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
           const bool in = lane < sh.leaves_last;
           leaf = in ? leaf : 0.0;
@@ -1135,304 +1021,6 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         md = moments_i128(D, T1, T2, T3, T4);
       }
       const double m2 = kssq / dn;
-      const double e = 2.220446049250313e-16 * md.mean;
-      const bool zd = m2 <= e * e;
-      const double sdd = sqrt(m2);
-      f64x2* o = reinterpret_cast<f64x2*>(out + (base + lane) * 8);
-      __builtin_nontemporal_store((f64x2){mp.mean, sdp}, o);
-      __builtin_nontemporal_store(
-          (f64x2){zp ? __builtin_nan("") : mp.m3 / (mp.m2 * sdp),
-                  zp ? __builtin_nan("") : mp.m4 / (mp.m2 * mp.m2) - 3.0}, o + 1);
-      __builtin_nontemporal_store((f64x2){md.mean, sdd}, o + 2);
-      __builtin_nontemporal_store(
-          (f64x2){zd ? __builtin_nan("") : md.m3 / (m2 * sdd),
-                  zd ? __builtin_nan("") : md.m4 / (m2 * m2) - 3.0}, o + 3);
-    }
-  }
-}
-
-// ---- DataBlock rows, teams of waves (round 4b) ----------------------------------------
-// lyon8_u8_dm (above) keeps a whole row in one wave's registers: 64 VGPRs of loads for a
-// two-chunk row, so at 128 VGPRs (4 waves/SIMD) the byte loop ran out of registers, chained
-// every byte's fma -> mul -> add through one temporary and waited for each word's LDS reads
-// before using them (SQ: VALU active 0.29, issue stalls 0.40 of wave cycles).  Here a row is
-// scored by a team of NCH waves, wave t taking numpy's chunk t (8192 values):
-//   * each wave holds 8 pieces (32 VGPRs) and stages its chunk into its own LDS image;
-//   * the integer row sum S1 (for the mean) is exchanged through LDS with one team barrier
-//     per row; the other exact sums and the chunk's sum of squared deviations stay with the
-//     wave, parked in lane (row mod 64), and are combined by wave 0 once per batch of 64 rows
-//     (chunk sums added in chunk order, as numpy);
-//   * the byte loop (dm_leaf_p) keeps eight independent fma / mul / add chains and issues the
-//     next word's LDS reads between a word's fma and its mul / add, so the reads' latency and
-//     the fp64 dependencies overlap.
-// NCH = 1 (rows <= 8192 bytes): four one-wave teams per block.
-// stage one chunk (the wave's 8 pieces) into its LDS image: full chunks at leaf lane/8 + 8j,
-// the row's last chunk where the block's table says (0xFFFF: past the chunk)
-__device__ __forceinline__ void dm_stage1(uint8_t* img, const u32x4 (&q)[8], int lane, bool last,
-                                          uint32_t full_base, const uint16_t* stab) {
-  typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;
-  if (!last) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      lds_u32* dst = (lds_u32*)(img + full_base + 1056 * j);
-      dst[0] = q[j].x;
-      dst[1] = q[j].y;
-      dst[2] = q[j].z;
-      dst[3] = q[j].w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t a0 = stab[(2 * j) * 64 + lane], a1 = stab[(2 * j + 1) * 64 + lane];
-      if (a0 != 0xFFFFu) {
-        lds_u32* dst = (lds_u32*)(img + a0);
-        dst[0] = q[j].x;
-        dst[1] = q[j].y;
-      }
-      if (a1 != 0xFFFFu) {
-        lds_u32* dst = (lds_u32*)(img + a1);
-        dst[0] = q[j].z;
-        dst[1] = q[j].w;
-      }
-    }
-  }
-}
-
-template <int NCH>
-struct DmTeam {
-  static constexpr int TEAM = NCH;                 // waves per row
-  static constexpr int WPB = NCH == 1 ? 4 : NCH;   // waves per block
-  static constexpr int TPB = WPB / TEAM;           // teams per block
-};
-
-#ifndef PFE_DMT_WPE
-#define PFE_DMT_WPE 4
-#endif
-#ifndef PFE_DMT_PREFETCH
-#define PFE_DMT_PREFETCH 1
-#endif
-template <int NCH, bool FPM>
-__global__ __launch_bounds__(64 * DmTeam<NCH>::WPB) __attribute__((amdgpu_waves_per_eu(PFE_DMT_WPE)))
-void lyon8_u8_dmt(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
-                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
-  static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
-  constexpr int TEAM = DmTeam<NCH>::TEAM, WPB = DmTeam<NCH>::WPB, TPB = DmTeam<NCH>::TPB;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[WPB][DM_IMG_BYTES];
-  __shared__ uint16_t stab[16 * 64];
-  __shared__ uint32_t xch[2][WPB];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int t = w % TEAM;  // the chunk this wave scores
-  const int tm = w / TEAM;
-  uint8_t* img = lds[w];
-  for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {  // as lyon8_u8_dm
-    const int jh = e >> 6, l = e & 63;
-    const int o = 16 * l + 1024 * (jh >> 1) + 8 * (jh & 1);
-    uint16_t a = 0xFFFFu;
-    if (o < sh.len_last) {
-      int L = 0;
-      while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
-      a = (uint16_t)(L * DM_S + (o - sh.start[L]));
-    }
-    stab[e] = a;
-  }
-  __syncthreads();
-  const int64_t nteams = (int64_t)gridDim.x * TPB;
-  const int64_t team = (int64_t)blockIdx.x * TPB + tm;
-  const int64_t r0 = n * team / nteams, r1 = n * (team + 1) / nteams;
-  const bool last = t == NCH - 1;
-  const int ppl = sh.lp >> 4;
-  int zpad = 0;  // zero bytes this lane reads past the row (last chunk only)
-#pragma unroll
-  for (int k = 0; k < 8; ++k) zpad += 8192 * t + 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
-  const uint32_t full_base = 16u * lane + 4u * (lane >> 3);
-  const int nw_last = lane < sh.leaves_last ? (sh.start[lane + 1] - sh.start[lane]) >> 3 : 16;
-  uint32_t z[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    z[j] = 0u;
-    asm volatile("" : "+v"(z[j]));
-  }
-  double sc = 0x1p1023;
-  asm volatile("" : "+s"(sc));
-  int par = 0;
-  // the wave's chunk of row c (8 x 16 B per lane) through a buffer descriptor of the row's ld
-  // bytes: pieces past the row read as zero bytes.  Row c + 1 is requested as soon as row
-  // c's pieces are staged, so its loads are in flight during row c's byte loop.
-  u32x4 q[8];
-  auto load_row = [&](int64_t c) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(dm + c * ds), 0, sh.ld, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      q[k] = __builtin_bit_cast(
-          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 8192 * t + 1024 * k, 2));
-  };
-  if (r0 < r1) load_row(r0);
-  for (int64_t base = r0; base < r1; base += 64) {
-    const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
-    uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
-    double kssq = 0.0;
-    for (int i = 0; i < cnt; ++i) {
-      const int64_t c = base + i;
-      if (!PFE_DMT_PREFETCH && i + base != r0) load_row(c);
-      Acc2 sd = {0, 0, 0, 0};
-      if constexpr (FPM) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          sd.s1 = __builtin_amdgcn_udot4(q[k].x, 0x01010101u, sd.s1, false);
-          sd.s1 = __builtin_amdgcn_udot4(q[k].y, 0x01010101u, sd.s1, false);
-          sd.s1 = __builtin_amdgcn_udot4(q[k].z, 0x01010101u, sd.s1, false);
-          sd.s1 = __builtin_amdgcn_udot4(q[k].w, 0x01010101u, sd.s1, false);
-        }
-      } else {
-#if defined(PFE_DM_PROBE) && (PFE_DM_PROBE & 2)  // timing probe: no power sums
-        sd.s1 = q[0].x + q[7].w;
-#else
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc2_x4(q[k], sd);
-#endif
-        sd.t3 += zpad << 21;
-        sd.t4 -= (uint64_t)zpad << 28;
-      }
-#if !(defined(PFE_DM_PROBE) && (PFE_DM_PROBE & 8))  // timing probe: no staging
-      dm_stage1(img, q, lane, last, full_base, stab);
-#else
-      if (q[3].x == 0x12345678u && q[5].y == 0x9abcdef0u) img[lane] = 1;
-#endif
-      if (PFE_DMT_PREFETCH) load_row(c + 1 < r1 ? c + 1 : c);  // (the last row again, unused)
-      const uint32_t S1t = wave_sum_u32(sd.s1);
-      uint32_t S1 = S1t;
-#if defined(PFE_DM_PROBE) && (PFE_DM_PROBE & 4)  // timing probe: no team barrier
-      if constexpr (false) {
-#else
-      if constexpr (TEAM > 1) {  // the row's S1 from the team (slots double-buffered by row)
-#endif
-        if (lane == 0) xch[par][w] = S1t;
-        __syncthreads();
-        S1 = 0;
-#pragma unroll
-        for (int u = 0; u < TEAM; ++u) S1 += xch[par][u];
-        par ^= 1;
-      }
-      const double mean = (double)S1 / (double)sh.ld;
-      const double nm = -__builtin_ldexp(mean, -51);
-      const bool mine = lane == i;
-      kS1 = mine ? S1 : kS1;
-      if constexpr (!FPM) {
-        const uint32_t S2 = wave_sum_u32(sd.s2);
-        const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
-        const uint32_t T3h = wave_sum_u32((uint32_t)(sd.t3 >> 16));
-        const uint32_t T4l = wave_sum_u32((uint32_t)sd.t4 & 0xFFFFFFu);
-        const uint32_t T4h = wave_sum_u32((uint32_t)(sd.t4 >> 24));
-        kS2 = mine ? S2 : kS2;
-        kT3l = mine ? T3l : kT3l;
-        kT3h = mine ? T3h : kT3h;
-        kT4l = mine ? T4l : kT4l;
-        kT4h = mine ? T4h : kT4h;
-      }
-      wave_lds_sync();
-      double l3 = 0.0, l4 = 0.0, leaf;
-#if defined(PFE_DM_PROBE) && (PFE_DM_PROBE & 1)  // timing probe: no byte loop
-      if (true) {
-        leaf = nm;
-      } else
-#endif
-      if (last) {
-        leaf = dm_leaf_p<FPM, true>(img + lane * DM_S, nm, sc, z, nw_last, l3, l4);
-        const bool in = lane < sh.leaves_last;
-        leaf = in ? leaf : 0.0;
-        l3 = in ? l3 : 0.0;
-        l4 = in ? l4 : 0.0;
-      } else {
-        leaf = dm_leaf_p<FPM, false>(img + lane * DM_S, nm, sc, z, 16, l3, l4);
-      }
-      const double cs = wave_sum_f64(leaf);  // numpy's tree over the chunk's leaves (x 2^-102)
-      if constexpr (FPM) {
-        const uint64_t b3 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(l3, 153)));
-        const uint64_t b4 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(l4, 204)));
-        kT3l = mine ? (uint32_t)b3 : kT3l;
-        kT3h = mine ? (uint32_t)(b3 >> 32) : kT3h;
-        kT4l = mine ? (uint32_t)b4 : kT4l;
-        kT4h = mine ? (uint32_t)(b4 >> 32) : kT4h;
-      }
-      kssq = mine ? cs : kssq;
-      wave_lds_sync();
-    }
-    // ---- combine the team's partial sums in wave 0 (through the other waves' images)
-    uint64_t S2 = kS2;
-    long long T3 = 0;
-    uint64_t T4 = 0;
-    double ssq = kssq, e3 = 0.0, e4 = 0.0;
-    if constexpr (FPM) {
-      e3 = __longlong_as_double((long long)(((uint64_t)kT3h << 32) | kT3l));
-      e4 = __longlong_as_double((long long)(((uint64_t)kT4h << 32) | kT4l));
-    } else {
-      T3 = (long long)(int)kT3h * 65536ll + (long long)kT3l;
-      T4 = ((uint64_t)kT4h << 24) + (uint64_t)kT4l;
-    }
-    if constexpr (TEAM > 1) {
-      typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;
-      __syncthreads();  // every wave's last reads of its image are done
-      if (t > 0) {
-        lds_u32* p = (lds_u32*)img;
-        const uint64_t sb = (uint64_t)__double_as_longlong(kssq);
-        p[0 * 64 + lane] = kS2;
-        p[1 * 64 + lane] = kT3l;
-        p[2 * 64 + lane] = kT3h;
-        p[3 * 64 + lane] = kT4l;
-        p[4 * 64 + lane] = kT4h;
-        p[5 * 64 + lane] = (uint32_t)sb;
-        p[6 * 64 + lane] = (uint32_t)(sb >> 32);
-      }
-      __syncthreads();
-      if (t == 0) {
-#pragma unroll
-        for (int u = 1; u < TEAM; ++u) {
-          const lds_u32* p = (const lds_u32*)lds[u];
-          const uint32_t s2 = p[0 * 64 + lane], t3l = p[1 * 64 + lane], t3h = p[2 * 64 + lane];
-          const uint32_t t4l = p[3 * 64 + lane], t4h = p[4 * 64 + lane];
-          const double cs = __longlong_as_double(
-              (long long)(((uint64_t)p[6 * 64 + lane] << 32) | p[5 * 64 + lane]));
-          ssq = ssq + cs;  // chunk sums in chunk order
-          if constexpr (FPM) {
-            e3 += __longlong_as_double((long long)(((uint64_t)t3h << 32) | t3l));
-            e4 += __longlong_as_double((long long)(((uint64_t)t4h << 32) | t4l));
-          } else {
-            S2 += s2;
-            T3 += (long long)(int)t3h * 65536ll + (long long)t3l;
-            T4 += ((uint64_t)t4h << 24) + (uint64_t)t4l;
-          }
-        }
-      }
-      __syncthreads();  // the images are free for the next batch
-    }
-    // ---- finalise the batch in wave 0: lane i -> row base + i
-    if (t == 0 && lane < cnt) {
-      Acc2 sp = {0, 0, 0, 0};
-      const u32x4* pr = reinterpret_cast<const u32x4*>(prof + (base + lane) * ps);
-      for (int k = 0; k < ppl; ++k) acc2_x4(__builtin_nontemporal_load(pr + k), sp);
-      const long long L = sh.lp;
-      const long long S1p = (long long)sp.s1;
-      const long long T1p = S1p - 128ll * L;
-      const long long T2p = (long long)sp.s2 - 256ll * S1p + 16384ll * L;
-      const Moments mp = moments_i64(L, T1p, T2p, (long long)sp.t3, sp.t4);
-      const double sdp = sqrt(mp.m2);
-      const bool zp = zero_var(mp);
-      const long long D = sh.ld;
-      const long long S1 = (long long)kS1;
-      const double dn = (double)D;
-      Moments md;
-      if constexpr (FPM) {
-        md.mean = (double)S1 / dn;
-        md.m3 = e3 / dn;
-        md.m4 = e4 / dn;
-      } else {
-        const long long T1 = S1 - 128ll * D;
-        const long long T2 = (long long)S2 - 256ll * S1 + 16384ll * D;
-        md = moments_i128(D, T1, T2, T3, T4);
-      }
-      const double m2 = __builtin_ldexp(ssq, 102) / dn;  // numpy's sum of squared deviations / n
       const double e = 2.220446049250313e-16 * md.mean;
       const bool zd = m2 <= e * e;
       const double sdd = sqrt(m2);
@@ -1582,14 +1170,14 @@ static bool dm_shape(int lp, int ld, DmShape& sh, int& nch) {
 }
 
 // blocks of K that fit on the device at once (occupancy x CUs), cached per kernel
-template <auto K, int THREADS = 256>
+template <auto K>
 static int resident_blocks() {
   static int cached[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
   if (cached[dev] > 0) return cached[dev];
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K), THREADS, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K), 256, 0) !=
           hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -1599,29 +1187,16 @@ static int resident_blocks() {
   return cached[dev];
 }
 
-template <int NCH, bool FPM, bool TAB = false>
+template <int NCH, bool FPM>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dm<NCH, FPM, TAB>;
+  constexpr auto K = lyon8_u8_dm<NCH, FPM>;
   int64_t blocks = resident_blocks<K>();
   const int64_t need = (n + 3) / 4;  // at least one row per wave
   if (blocks > need) blocks = need;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(K, dim3((unsigned)blocks), dim3(256), 0, st, prof, ps, dm, ds, n, out, sh);
-}
-
-template <int NCH, bool FPM>
-static void launch_dmt_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
-                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dmt<NCH, FPM>;
-  constexpr int WPB = DmTeam<NCH>::WPB, TPB = DmTeam<NCH>::TPB;
-  int64_t blocks = resident_blocks<K, 64 * WPB>();
-  const int64_t need = (n + TPB - 1) / TPB;  // at least one row per team
-  if (blocks > need) blocks = need;
-  if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(K, dim3((unsigned)blocks), dim3(64 * WPB), 0, st, prof, ps, dm, ds, n, out, sh);
 }
 
 hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_t* dm,
@@ -1634,46 +1209,23 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
   int dnch = 0;
   if (o.lyon8_dm != 1 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
       ld != 16384 && dm_shape(lp, ld, dsh, dnch)) {
-    // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dmt (teams
-    // of waves; option 2: its fp64-moment variant), option 3: the one-wave lyon8_u8_dm
+    // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dm (DESIGN
+    // §3.1c), skew / kurt from fp64 d^3 / d^4 sums for rows of one or two numpy chunks (nDM <=
+    // 128, the faster of the two measured there), from the exact power sums beyond and with
+    // option 2 everywhere
     const int cap = o.lyon8_blocks;
-    if (o.lyon8_dm == 5 && dnch <= 2) {  // one wave per row, tabulated squares
-      if (dnch == 1)
-        launch_dm_kernel<1, false, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
-      else
-        launch_dm_kernel<2, false, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
-      return hipGetLastError();
-    }
-    if (o.lyon8_dm == 4 && dnch <= 2) {  // one wave per row, fp64 d^3 / d^4 moments
+    if (o.lyon8_dm == 0 && dnch <= 2) {
       if (dnch == 1)
         launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
       else
         launch_dm_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
-      return hipGetLastError();
-    }
-    if (o.lyon8_dm == 3) {
+    } else {
       switch (dnch) {
         case 1: launch_dm_kernel<1, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
         case 2: launch_dm_kernel<2, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
         case 3: launch_dm_kernel<3, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
         default: launch_dm_kernel<4, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
       }
-      return hipGetLastError();
-    }
-    if (o.lyon8_dm == 2) {
-      switch (dnch) {
-        case 1: launch_dmt_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-        case 2: launch_dmt_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-        case 3: launch_dmt_kernel<3, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-        default: launch_dmt_kernel<4, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-      }
-      return hipGetLastError();
-    }
-    switch (dnch) {
-      case 1: launch_dmt_kernel<1, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-      case 2: launch_dmt_kernel<2, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-      case 3: launch_dmt_kernel<3, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-      default: launch_dmt_kernel<4, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
     }
     return hipGetLastError();
   }

@@ -16,7 +16,7 @@ struct Options {
   int lyon8_blocks = 16384;        // grid cap of the Lyon-8 stream kernel
   int lyon8_burst = 2;             // candidate groups per wave step of the Lyon-8 kernel
   int pfd_waves = 4;               // waves per fold of the PFD dmprof kernel (4 or 1)
-  int lyon8_dm = 0;                // DataBlock DM rows: 0 lyon8_u8_dmt, 1 round 3, 2 FPM, 3 lyon8_u8_dm
+  int lyon8_dm = 0;                // DataBlock DM rows (pfe.h PFE_OPT_LYON8_DM, 0..2)
   int pfd_split = 0;               // PFD dmprof: 1 part sums by k_pfd_parts beside the sweep, 0 fused
 };
 
