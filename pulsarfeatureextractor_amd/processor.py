@@ -246,9 +246,10 @@ def _cuts(n, batch):
     return [0] + np.cumsum(sizes).tolist()
 
 
-def _stream(paths, parse, score, emit, batch=BATCH, depth=1):
-    """parse(batch paths) on a helper thread, ahead of the GPU stage; score(parsed, slot) of
-    batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
+def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3):
+    """parse(batch paths) on a helper thread, up to `ahead` batches beyond those being scored
+    (the parser never waits for a GPU step unless it is that far ahead); score(parsed, slot)
+    of batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
     once, each on its own engine handle and pinned slabs); emit(batch offset, batch paths,
     results) on the calling thread in discovery order, overlapping the next batches'
     scoring."""
@@ -275,14 +276,14 @@ def _stream(paths, parse, score, emit, batch=BATCH, depth=1):
                     f = parsed.pop(k)
                     scored[k] = slots[k % depth].submit(lambda f=f, k=k: score(f.result(), k % depth))
 
-            for k in range(min(depth + 1, nb)):
+            for k in range(min(depth + ahead, nb)):
                 submit_parse(k)
             for k in range(min(depth, nb)):
                 submit_score(k)
             for k in range(nb):
                 res = scored.pop(k).result()
                 submit_score(k + depth)
-                submit_parse(k + depth + 1)
+                submit_parse(k + depth + ahead)
                 emit(cuts[k], part(k), res)
     finally:
         for ex in slots:
@@ -391,8 +392,12 @@ class RunMetrics:
         self.t0 = time.perf_counter()
         self.parse_s = 0.0
         self.score_s = 0.0
+        self.stage = {}  # finer host timers of the GPU stage (pack, gpu), summed over slots
         self.batches = 0
         self.reasons = {}
+
+    def add(self, key, dt):
+        self.stage[key] = self.stage.get(key, 0.0) + dt
 
     def timed_parse(self, fn):
         def wrapped(paths):
@@ -426,7 +431,8 @@ class RunMetrics:
                 "failures_by_reason": dict(sorted(self.reasons.items())),
                 "batches": self.batches, "wall_s": round(wall, 6),
                 "candidates_per_s": round(processed / wall, 3) if wall > 0 else None,
-                "parse_s": round(self.parse_s, 6), "score_s": round(self.score_s, 6)}
+                "parse_s": round(self.parse_s, 6), "score_s": round(self.score_s, 6),
+                **{k + "_s": round(v, 6) for k, v in sorted(self.stage.items())}}
 
 
 class DataProcessor:
@@ -440,6 +446,7 @@ class DataProcessor:
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
                  start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2):
         self.debug = debugFlag
+        self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
         self.metrics = None   # RunMetrics.as_dict() of the last mode run
         self.engine = engine
@@ -566,10 +573,12 @@ class DataProcessor:
             for s0 in range(0, len(rows), self.gpu_batch):
                 r = rows[s0:s0 + self.gpu_batch]
                 m, dst = len(r), px[r]
+                t0 = time.perf_counter()
                 a = pre.nb.pack(r, lp=lp, nsub_lsb=(nsub, lsb), ndm=ndm, alloc=sl.view,
                                 threads=self.workers)
                 o = sl.view("out22", (m, 22), np.float64)
                 st = sl.view("status", (m,), np.uint32)
+                t1 = time.perf_counter()
                 try:
                     self._eng(slot).bates22(a["prof"], a["sub"], a["dmcurve"], a["scal"], out=o,
                                         status=st)
@@ -577,6 +586,10 @@ class DataProcessor:
                     for d in dst:
                         err[d] = f"Exception: {e}"
                     continue
+                finally:
+                    if self._run is not None:
+                        self._run.add("pack", t1 - t0)
+                        self._run.add("gpu", time.perf_counter() - t1)
                 mat[dst] = o
                 for j in np.flatnonzero(st & 0xFF):
                     err[dst[j]] = status_error(int(st[j]))
@@ -694,8 +707,16 @@ class DataProcessor:
         from ._native import format_rows
 
         counts = {"ok": 0, "failed": 0}
+        self._run = run
 
         def emit(off, batch_paths, res):
+            t0 = time.perf_counter()
+            try:
+                _emit(off, batch_paths, res)
+            finally:
+                run.add("emit", time.perf_counter() - t0)
+
+        def _emit(off, batch_paths, res):
             nfail = sum(1 for e in res.err if e)
             counts["failed"] += nfail
             counts["ok"] += len(batch_paths) - nfail

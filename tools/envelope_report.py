@@ -5,7 +5,7 @@ for every golden set and LM score, the rows where the reference's K = 50 samples
 wide rows the GPU value falls outside, and the binomial bound the test applies
 (golden_util.envelope_check).
 
-  python tools/envelope_report.py gpurun_out/r03_golden_gpu.npz > profiles/r03_envelope_rows.txt
+  python tools/envelope_report.py gpurun_out/r04_golden_gpu.npz > profiles/r04_envelope_rows.txt
 """
 import os
 import sys
@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from golden_util import envelope_check  # noqa: E402
 
 BITEXACT = (2, 3, 11, 12, 13, 14, 15, 19, 21)
-SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide")
+SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide",
+        "bates22_phcx128_big", "bates22_superb64_big", "label_phcx")
 
 
 def main():

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """GPU scores of the golden Bates sets (current build, default solver) for host-side reports:
 
-  python tools/golden_dump.py gpurun_out/r03_golden_gpu.npz          (on the GPU box)
-  python tools/envelope_report.py gpurun_out/r03_golden_gpu.npz      (here)
+  python tools/golden_dump.py gpurun_out/r04_golden_gpu.npz          (on the GPU box)
+  python tools/envelope_report.py gpurun_out/r04_golden_gpu.npz      (here)
 """
 import os
 import sys
@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from golden_util import bates_inputs, load  # noqa: E402
 from pulsarfeatureextractor_amd._native import Engine  # noqa: E402
 
-SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide")
+SETS = ("bates22_phcx128", "bates22_superb64", "all30_phcx128", "bates22_phcx128_wide",
+        "bates22_phcx128_big", "bates22_superb64_big", "label_phcx")
 
 
 def main():

@@ -18,6 +18,7 @@
 #   pmc_l8dm     FETCH_SIZE / WRITE_SIZE passes of the nDM = 120 command
 #   sq_l8dm      two SQ counter passes over the nDM = 120 kernel + tools/sq_summary.py
 #   e2e          tools/e2e_bench.py --mode stream on 50 000 synthetic PHCX files
+#   golden_dump  the 22 scores of every golden set (tools/golden_dump.py; host: envelope_report)
 #   pfdab        bench.py --path pfd with the split pipeline (default) and fused (pfd_split=0)
 #   pytest:<f>   one test file, e.g. pytest:tests/test_lyon8_gpu.py
 set -o pipefail
@@ -94,6 +95,9 @@ for step in "$@"; do
     e2e)
       timeout -k 10 600 python -u tools/e2e_bench.py --mode stream --n 50000 --dir /tmp/pfe_e2e \
         --depth ${E2E_DEPTH:-1,2} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;
+    golden_dump)
+      timeout -k 10 300 python -u tools/golden_dump.py $O/${T}_golden_gpu.npz > $O/${T}_golden_dump.log 2>&1 \
+        || fail golden_dump $O/${T}_golden_dump.log ;;
     pfdab)
       for v in 1 0; do
         timeout -k 10 300 python3 bench.py --path pfd --steps 10 --warmup 2 --no-cpu-baseline \
