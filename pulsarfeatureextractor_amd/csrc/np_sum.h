@@ -11,7 +11,7 @@ namespace pfe {
 // ---- numpy pairwise summation ---------------------------------------------------------
 // a leaf (n <= 128): r[j] = a[j] + a[j+8] + ... over the largest multiple of 8, combined as
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the remainder in order; n < 8: 0 + a0 + a1 ...
-__device__ double np_leaf(const double* a, int n, int lane) {
+__device__ __forceinline__ double np_leaf(const double* a, int n, int lane) {
   if (n < 8) {
     double r = 0.0;
     for (int i = 0; i < n; ++i) r += a[i];
@@ -58,6 +58,18 @@ __device__ __noinline__ double np_pairwise(const double* a, int n, int lane) {
 template <>
 __device__ __noinline__ double np_pairwise<0>(const double* a, int n, int lane) {
   return np_leaf(a, n, lane);
+}
+
+// np_pairwise with every level inlined (no call): exact for n <= 128 * 2^D
+template <int D>
+__device__ __forceinline__ double np_pairwise_inl(const double* a, int n, int lane) {
+  if (n <= 128 || D == 0) return np_leaf(a, n, lane);
+  if constexpr (D > 0) {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise_inl<D - 1>(a, n2, lane) + np_pairwise_inl<D - 1>(a + n2, n - n2, lane);
+  }
+  return 0.0;
 }
 
 // float32 pairwise sum of a short array (n <= 128), evaluated identically in every lane

@@ -34,8 +34,16 @@ __device__ __forceinline__ double delay_from_dm(double dm, double f) {  // PFDOp
 
 // numpy's pairwise sum of an LDS row with the leaf's loads issued before its adds when the
 // row is a single leaf (np_leaf128: the same order of additions, so the same bits)
+// NC (the four-wave kernel, rows of <= 1024 values): every level inlined, no call -- a call
+// in a kernel makes the backend assume the callee's register needs (212 VGPRs and 2 waves per
+// SIMD for k_pfd_dmprof4 with the recursive call in it, 123 without)
+template <bool NC = false>
 __device__ __forceinline__ double np_sum_row(const double* a, int n, int lane) {
-  return (n >= 8 && n <= 128) ? np_leaf128(a, n, lane) : np_pairwise<12>(a, n, lane);
+  if (n >= 8 && n <= 128) return np_leaf128(a, n, lane);
+  if constexpr (NC)
+    return np_pairwise_inl<3>(a, n, lane);
+  else
+    return np_pairwise<12>(a, n, lane);
 }
 
 // Python's builtin min (MAX = false) / max over an LDS row as a wave reduction: a[0] when
@@ -43,7 +51,7 @@ __device__ __forceinline__ double np_sum_row(const double* a, int n, int lane) {
 // sequential scan with strict comparisons returns (py_min_seq / py_max_seq), ties and the
 // sign of zero included, since the pair (value, first index) is carried
 template <bool MAX>
-__device__ double py_ext_wave(const double* a, int n, int lane) {
+__device__ __forceinline__ double py_ext_wave(const double* a, int n, int lane) {
   const double a0 = a[0];
   if (!(a0 == a0)) return a0;
   double bv = a0;
@@ -69,7 +77,7 @@ __device__ double py_ext_wave(const double* a, int n, int lane) {
 
 // numpy's float32 leaf sum of a short LDS row (np_leaf_f32) with the 8 accumulators in lanes
 // 0-7: the same additions in the same order, the result in every lane
-__device__ float np_leaf_f32_wave(const float* a, int n, int lane) {
+__device__ __forceinline__ float np_leaf_f32_wave(const float* a, int n, int lane) {
   if (n < 8) return np_leaf_f32(a, n);
   const int nb = n - (n % 8);
   float r = 0.0f;
@@ -87,21 +95,22 @@ __device__ float np_leaf_f32_wave(const float* a, int n, int lane) {
 
 // mean, std, skew, kurtosis of x[0..n) (LDS) as numpy.mean / numpy.std / scipy.stats.skew /
 // scipy.stats.kurtosis compute them in float64; tmp: n doubles of LDS scratch
-__device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double (&o)[4]) {
-  const double mean = np_sum_row(x, n, lane) / (double)n;
+template <bool NC>
+__device__ __forceinline__ void stats4_f64(const double* x, double* tmp, int n, int lane, double (&o)[4]) {
+  const double mean = np_sum_row<NC>(x, n, lane) / (double)n;
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
     tmp[i] = d * d;
   }
   lds_sync();
-  const double m2 = np_sum_row(tmp, n, lane) / (double)n;
+  const double m2 = np_sum_row<NC>(tmp, n, lane) / (double)n;
   lds_sync();
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
     tmp[i] = (d * d) * d;
   }
   lds_sync();
-  const double m3 = np_sum_row(tmp, n, lane) / (double)n;
+  const double m3 = np_sum_row<NC>(tmp, n, lane) / (double)n;
   lds_sync();
   for (int i = lane; i < n; i += 64) {
     const double d = x[i] - mean;
@@ -109,7 +118,7 @@ __device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double
     tmp[i] = d2 * d2;
   }
   lds_sync();
-  const double m4 = np_sum_row(tmp, n, lane) / (double)n;
+  const double m4 = np_sum_row<NC>(tmp, n, lane) / (double)n;
   lds_sync();
   const double eps = 2.220446049250313e-16;
   const double zl = eps * mean;
@@ -122,7 +131,7 @@ __device__ void stats4_f64(const double* x, double* tmp, int n, int lane, double
 
 // the same in float32 (numpy on a float32 array): the element passes spread over the lanes,
 // the leaf sums in lanes 0-7, the result in every lane
-__device__ void stats4_f32_wave(const float* a, float* tmp, int n, int lane, double (&o)[4]) {
+__device__ __forceinline__ void stats4_f32_wave(const float* a, float* tmp, int n, int lane, double (&o)[4]) {
   const float mean = np_leaf_f32_wave(a, n, lane) / (float)n;
   for (int i = lane; i < n; i += 64) {
     const float d = a[i] - mean;
@@ -163,7 +172,7 @@ __device__ __forceinline__ double filter_neg_pfd(double v) {
 // numpy.argmax over i of a[(i + shift) mod n] - sub (|shift| < n) as a wave reduction: the
 // first NaN if there is one, else the first maximum (the values are the same roundings a
 // sequential scan compares; ties go to the smaller i, so +0 / -0 ties too)
-__device__ int np_argmax_wave(const double* a, int n, int shift, double sub, int lane) {
+__device__ __forceinline__ int np_argmax_wave(const double* a, int n, int shift, double sub, int lane) {
   int nan_i = 1 << 30, bi = 1 << 30;
   double bv = 0.0;
   for (int i = lane; i < n; i += 64) {
@@ -198,15 +207,16 @@ __device__ int np_argmax_wave(const double* a, int n, int shift, double sub, int
 // rotates with fft_rotate (:490-500) by an integer number of bins; this is the exact
 // rotation, which pocketfft's round-off (~1e-13) can differ from only when a bin lies within
 // that of the half maximum.
-__device__ void pfd_params(const double* prof, double* tmp, int L, int lane, double& snr,
+template <bool NC>
+__device__ __forceinline__ void pfd_params(const double* prof, double* tmp, int L, int lane, double& snr,
                            double& width) {
-  const double avg = np_sum_row(prof, L, lane) / (double)L;          // :130
+  const double avg = np_sum_row<NC>(prof, L, lane) / (double)L;          // :130
   for (int b = lane; b < L; b += 64) {
     const double d = prof[b] - avg;
     tmp[b] = d * d;
   }
   lds_sync();
-  const double var = np_sum_row(tmp, L, lane) / (double)L;          // :131
+  const double var = np_sum_row<NC>(tmp, L, lane) / (double)L;          // :131
   lds_sync();
   const double sigma = sqrt(var);
   const double lo = avg - 3.0 * sigma, hi = avg + 3.0 * sigma;
@@ -219,19 +229,19 @@ __device__ void pfd_params(const double* prof, double* tmp, int L, int lane, dou
     m += __popcll(bal);
   }
   lds_sync();
-  const double avg2 = np_sum_row(tmp, m, lane) / (double)m;         // :148 (empty: NaN)
+  const double avg2 = np_sum_row<NC>(tmp, m, lane) / (double)m;         // :148 (empty: NaN)
   lds_sync();
   for (int i = lane; i < m; i += 64) {
     const double d = tmp[i] - avg2;
     tmp[i] = d * d;
   }
   lds_sync();
-  const double var2 = np_sum_row(tmp, m, lane) / (double)m;         // :149
+  const double var2 = np_sum_row<NC>(tmp, m, lane) / (double)m;         // :149
   lds_sync();
   const double sd2 = sqrt(var2);
   for (int b = lane; b < L; b += 64) tmp[b] = (prof[b] - avg2) / sd2;
   lds_sync();
-  snr = np_sum_row(tmp, L, lane);                                    // :151
+  snr = np_sum_row<NC>(tmp, L, lane);                                    // :151
   lds_sync();
   if (snr < 0.0) snr = 0.1;                                              // :152-153
   // width (:194-231): the sequential scans of the reference as wave reductions over the
@@ -315,11 +325,12 @@ __device__ __forceinline__ double sum8(double v) {
 // sub-band profiles T (nsub x L, profs.sum(0), PFDFile.plot_subbands :442-456) and s22 from
 // getProfileCorr (:445-466).  T is overwritten (boxcar sums).  mb, mean, var: nsub doubles.
 // false = the reference raises (max_bin unbound, width_bins == 0, no valid pair).
-__device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, double* mb,
+template <bool NC>
+__device__ __forceinline__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, double* mb,
                                    double* bmean, double* bvar, int NS, int L, int lane,
                                    double width, double (&o)[3]) {
   // s22 first, while T holds the sub-band profiles
-  const double pm = np_sum_row(prof, L, lane) / (double)L;
+  const double pm = np_sum_row<NC>(prof, L, lane) / (double)L;
   for (int b = lane; b < L; b += 64) tmp[b] = prof[b] - pm;
   lds_sync();
   const double inv2 = 1.0 / (double)(L - 1);
@@ -349,7 +360,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   } else {
     for (int j = 0; j < NS; ++j) {
       const double* r = T + (size_t)j * L;
-      const double mj = np_sum_row(r, L, lane) / (double)L;
+      const double mj = np_sum_row<NC>(r, L, lane) / (double)L;
       double dl_ = 0.0, ql_ = 0.0;  // wdot's order for both sums, in one pass
       for (int b = lane; b < L; b += 64) {
         const double e = r[b] - mj;
@@ -484,7 +495,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
     lds_sync();
   }
   // RMS scatter of the maxima (:1629-1651)
-  const double med = np_sum_row(mb, NS, lane) / (double)NS;
+  const double med = np_sum_row<NC>(mb, NS, lane) / (double)NS;
   int count = 0;
   double var_med = 0.0;
   for (int i = 0; i < NS; ++i)
@@ -528,7 +539,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
   } else {
     for (int i = 0; i < NS; ++i) {
       double* r = T + (size_t)i * L;
-      const double m = np_sum_row(r, nw, lane) / (double)nw;
+      const double m = np_sum_row<NC>(r, nw, lane) / (double)nw;
       lds_sync();
       for (int j = lane; j < nw; j += 64) r[j] = r[j] - m;
       lds_sync();
@@ -592,6 +603,7 @@ __device__ bool pfd_subband_scores(double* T, const double* prof, double* tmp, d
 
 // the rest of a fold after the chi^2 sweep (one wave): DM-curve statistics, the 22-score
 // parameters and sub-band scores, status
+template <bool NC>
 __device__ __forceinline__ void pfd_finish(const PfdArgs& a, int64_t c, double* T, double* buf,
                                         double* tmp, double* dl, double* sdb, double* bv,
                                         float* chs, float* ftmp, const double (&po)[4],
@@ -614,13 +626,13 @@ __device__ __forceinline__ void pfd_finish(const PfdArgs& a, int64_t c, double* 
   uint32_t st = dm_ok ? 0u : PFE_ST_PFD_DMCURVE_FAIL;
   if (a.out22) {
     double snr, width;
-    pfd_params(buf, tmp, L, lane, snr, width);
+    pfd_params<NC>(buf, tmp, L, lane, snr, width);
     const double period = sc[PFE_PFD_BARY_P1] * 1000.0;            // PFDOperations.py:127
     const double span1 = dm_lo + ((dm_hi - dm_lo) * 1.0) / (double)(PFE_PFD_NDM - 1);
     const double span_last =
         dm_lo + ((dm_hi - dm_lo) * (double)(PFE_PFD_NDM - 1)) / (double)(PFE_PFD_NDM - 1);
     double sb[3];
-    const bool sb_ok = pfd_subband_scores(T, buf, tmp, dl, sdb, bv, NS, L, lane, width, sb);
+    const bool sb_ok = pfd_subband_scores<NC>(T, buf, tmp, dl, sdb, bv, NS, L, lane, width, sb);
     if (!sb_ok) st |= PFE_ST_SUBBAND_FAIL;
     if (lane == 0) {
       double* o = a.out22 + c * 22;
@@ -701,7 +713,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
     const double mn = py_ext_wave<false>(buf, L, lane);
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] - mn;  // normprof
     lds_sync();
-    const double mean = np_sum_row(buf, L, lane) / (double)L;
+    const double mean = np_sum_row<false>(buf, L, lane) / (double)L;
     lds_sync();
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] / mean;  // s
     lds_sync();
@@ -715,7 +727,7 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
     lds_sync();
   }
   double po[4] = {0.0, 0.0, 0.0, 0.0};
-  if (a.lyon8) stats4_f64(buf, tmp, L, lane, po);
+  if (a.lyon8) stats4_f64<false>(buf, tmp, L, lane, po);
   // ---- chi^2 versus DM over span(dms[0], dms[-1], 100) (PFDFile.py:378-423)
   const bool dm_ok = numdms > 1.0;  // numdms == 1: dms is a scalar and dms[0] raises
   if (dm_ok && (a.chis || a.lyon8)) {
@@ -752,14 +764,14 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
     }
     lds_sync();
   }
-  pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
+  pfd_finish<false>(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
-constexpr int PFD4_E = 16;  // fold elements per thread and load step of k_pfd_dmprof4
+constexpr int PFD4_E = 8;  // fold elements per thread and load step of k_pfd_dmprof4 (126 VGPRs)
 
 // the accumulated sub-band rotations of the 100 trial DMs (PFDFile.py:395-416), one lane
 // per sub-band: rot[k][j] (the sweep of the single-wave kernel keeps them in cum / sdb)
-__device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, const double* fr,
+__device__ __forceinline__ void sweep_rotations(uint16_t* rot, const double* sdb, const double* fr,
                                                 int NS, int L, double bps, double dm_lo,
                                                 double dm_hi, int lane) {
   for (int j = lane; j < NS; j += 64) {
@@ -772,7 +784,7 @@ __device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, con
       const double nw = floor(delaybins + 0.5);
       cu = pymod((long long)cu + (long long)nw, L);
       sd = sd + nw;
-      rot[k * NS + j] = cu;
+      rot[k * NS + j] = (uint16_t)cu;  // 0 <= cu < L <= 128
     }
   }
 }
@@ -785,7 +797,7 @@ __device__ __forceinline__ void sweep_rotations(int* rot, const double* sdb, con
 // independent ordered chains per lane.  numpy's pairwise leaf of the two chi^2 rows runs in
 // lanes 0-7 (DM k) and 8-15 (DM k + 4) together.
 template <int L>
-__device__ __forceinline__ void sweep_pow2(const double* T, const int* rot, int NS, int wv,
+__device__ __forceinline__ void sweep_pow2(const double* T, const uint16_t* rot, int NS, int wv,
                                            int lane, double avgprof, double varprof,
                                            double* xb, float* chs, float* chis) {
   constexpr int B = L / 64;  // bins per lane
@@ -793,33 +805,38 @@ __device__ __forceinline__ void sweep_pow2(const double* T, const int* rot, int 
   for (int k0 = wv; k0 < PFE_PFD_NDM; k0 += 8) {
     const bool two = k0 + 4 < PFE_PFD_NDM;  // wave-uniform
     const int k1 = two ? k0 + 4 : k0;
-    const int* ra = rot + k0 * NS;
-    const int* rb = rot + k1 * NS;
+    const uint16_t* ra = rot + k0 * NS;
+    const uint16_t* rb = rot + k1 * NS;
     double s[2][B];
     for (int j0 = 0; j0 < NS; j0 += 8) {
-      const int rv = lane < 8 ? ra[j0 + lane] : lane < 16 ? rb[j0 + lane - 8] : 0;
-      double v[2][8][B];
+      const int rv = lane < 8 ? (int)ra[j0 + lane] : lane < 16 ? (int)rb[j0 + lane - 8] : 0;
+      // two halves of 4 sub-bands (the same adds in the same order as one step of 8; half
+      // the registers for the row reads in flight)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r0 = __builtin_amdgcn_readlane(rv, u);
-        const int r1 = __builtin_amdgcn_readlane(rv, 8 + u);
-        const double* row = T + (size_t)(j0 + u) * L;
+      for (int h = 0; h < 2; ++h) {
+        double v[2][4][B];
 #pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const int b = lane + 64 * q;
-          v[0][u][q] = row[(b + r0) & (L - 1)];
-          v[1][u][q] = row[(b + r1) & (L - 1)];
+        for (int u = 0; u < 4; ++u) {
+          const int r0 = __builtin_amdgcn_readlane(rv, 4 * h + u);
+          const int r1 = __builtin_amdgcn_readlane(rv, 8 + 4 * h + u);
+          const double* row = T + (size_t)(j0 + 4 * h + u) * L;
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            const int b = lane + 64 * q;
+            v[0][u][q] = row[(b + r0) & (L - 1)];
+            v[1][u][q] = row[(b + r1) & (L - 1)];
+          }
         }
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            double t = (j0 == 0 && h == 0) ? v[d][0][q] : s[d][q] + v[d][0][q];
+#pragma unroll
+            for (int u = 1; u < 4; ++u) t = t + v[d][u][q];
+            s[d][q] = t;
+          }
       }
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-          double t = j0 == 0 ? v[d][0][q] : s[d][q] + v[d][0][q];
-#pragma unroll
-          for (int u = 1; u < 8; ++u) t = t + v[d][u][q];
-          s[d][q] = t;
-        }
     }
     // chi^2 terms of both DMs, then numpy's leaf: r_i = x[i] + x[i+8] + ... (L multiple of 8)
 #pragma unroll
@@ -866,7 +883,7 @@ __device__ __forceinline__ void sweep_pow2(const double* T, const int* rot, int 
 //     conflict-free) and numpy's pairwise leaf sums the chi^2 terms;
 //   * wave 0 builds the profile and finishes the fold (statistics, 22-score parameters) as
 //     the single-wave kernel.
-__global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_pfd_dmprof4(PfdArgs a) {
   extern __shared__ double lds[];
   const int64_t c = blockIdx.x;
   if (c >= a.n) return;
@@ -881,8 +898,8 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
   double* sdb = dl + NS;             // NS
   double* bv = sdb + NS;             // NS
   int* cum = (int*)(bv + NS);        // NS
-  int* rot = cum + NS;               // PFE_PFD_NDM x NS accumulated rotations of the sweep
-  double* xbuf = bv + NS + ((PFE_PFD_NDM + 1) * NS + 1) / 2;  // 4 x 256, after cum and rot
+  uint16_t* rot = (uint16_t*)(cum + NS);  // PFE_PFD_NDM x NS accumulated rotations (< L)
+  double* xbuf = bv + NS + (4 * NS + 2 * PFE_PFD_NDM * NS + 7) / 8;  // 4 x 256, after cum, rot
   __shared__ float chs[PFE_PFD_NDM], ftmp[PFE_PFD_NDM];
   const double* sc = a.scal + c * PFE_PFD_NSCAL;
   const double bestdm = sc[PFE_PFD_BESTDM], bps = sc[PFE_PFD_BINSPERSEC];
@@ -968,7 +985,7 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
     double* xb = xbuf + wv * 256;
     const int b0 = lane, b1 = lane + 64;
     for (int k = wv; k < PFE_PFD_NDM; k += 4) {
-      const int* rk = rot + k * NS;
+      const uint16_t* rk = rot + k * NS;
       // 8 sub-bands per step: their rotations, then all 16 row reads, then the ordered adds
       // (unconditional reads at clamped indices keep every load of a step in flight)
       double s0 = 0.0, s1 = 0.0;
@@ -1031,7 +1048,7 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
     const double mn = py_ext_wave<false>(buf, L, lane);
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] - mn;  // normprof
     lds_sync();
-    const double mean = np_sum_row(buf, L, lane) / (double)L;
+    const double mean = np_sum_row<true>(buf, L, lane) / (double)L;
     lds_sync();
     for (int b = lane; b < L; b += 64) buf[b] = buf[b] / mean;  // s
     lds_sync();
@@ -1043,9 +1060,9 @@ __global__ __launch_bounds__(256, 2) void k_pfd_dmprof4(PfdArgs a) {
       if (a.profile) a.profile[c * L + b] = buf[b];
     }
     lds_sync();
-    if (a.lyon8) stats4_f64(buf, tmp, L, lane, po);
+    if (a.lyon8) stats4_f64<true>(buf, tmp, L, lane, po);
   }
-  pfd_finish(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
+  pfd_finish<true>(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
 // Split pipeline, stage 1: the fold's part sums T (as k_pfd_dmprof4 reduces them: the
@@ -1114,12 +1131,18 @@ size_t pfd_lds_bytes(int nsub, int L) {
 }
 
 static size_t pfd4_lds_bytes(int nsub, int L) {
-  return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(int) + 8 +
+  return pfd_lds_bytes(nsub, L) + (size_t)PFE_PFD_NDM * nsub * sizeof(uint16_t) + 8 +
          4 * 256 * sizeof(double);
 }
 
+// the four-wave kernel: <= 128 bins, the fold in LDS, and rows of <= 1024 values (its
+// pairwise sums are inlined three levels deep, np_sum_row<true>)
+static bool pfd4_ok(const PfdArgs& a) {
+  return a.L <= 128 && a.nsub <= 1024 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4;
+}
+
 bool pfd_split_ok(const PfdArgs& a) {
-  return a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4;
+  return pfd4_ok(a);
 }
 
 // the folds [c0, c0 + cn) of a batch: every per-fold pointer moved to fold c0
@@ -1170,7 +1193,7 @@ hipError_t launch_pfd_dmprof_split(const PfdArgs& a, hipStream_t st, hipStream_t
 }
 
 hipError_t launch_pfd_dmprof(const PfdArgs& a, hipStream_t st) {
-  if (a.L <= 128 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4) {
+  if (pfd4_ok(a)) {
     const size_t lds4 = pfd4_lds_bytes(a.nsub, a.L);
     hipError_t e = ensure_dyn_lds<k_pfd_dmprof4>(lds4);
     if (e != hipSuccess) return e;

@@ -230,23 +230,23 @@ def score_lyon8(cands, engine=None):
     return out
 
 
-def _cuts(n, batch):
+def _cuts(n, batch, ramp=True):
     """Batch boundaries of a streamed run: full batches, except that a long run starts and
     ends with batch/8, batch/4, batch/2 so the GPU stage starts after a short first parse and
     the last batch's scoring and output trail the last parse by little."""
-    ramp = [batch // 8, batch // 4, batch // 2]
-    if batch < 64 or n < 2 * sum(ramp) + batch:
+    steps = [batch // 8, batch // 4, batch // 2]
+    if not ramp or batch < 64 or n < 2 * sum(steps) + batch:
         return list(range(0, n, batch)) + [n]
-    sizes = list(ramp)
-    rem = n - 2 * sum(ramp)
+    sizes = list(steps)
+    rem = n - 2 * sum(steps)
     while rem > 0:
         sizes.append(min(batch, rem))
         rem -= sizes[-1]
-    sizes += ramp[::-1]
+    sizes += steps[::-1]
     return [0] + np.cumsum(sizes).tolist()
 
 
-def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3):
+def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3, ramp=True):
     """parse(batch paths) on a helper thread, up to `ahead` batches beyond those being scored
     (the parser never waits for a GPU step unless it is that far ahead); score(parsed, slot)
     of batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
@@ -255,7 +255,7 @@ def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3):
     scoring."""
     if not paths:
         return
-    cuts = _cuts(len(paths), batch)
+    cuts = _cuts(len(paths), batch, ramp)
     nb = len(cuts) - 1
 
     def part(k):
@@ -444,7 +444,7 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2):
+                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True):
         self.debug = debugFlag
         self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
@@ -465,6 +465,7 @@ class DataProcessor:
         # gpu_depth batches are scored at once (processor._stream), each slot with its own
         # engine handle (stream + workspace) and pinned slabs
         self.depth = max(1, int(gpu_depth))
+        self.ramp = bool(ramp)  # ramped batch sizes at both ends of a streamed run (_cuts)
         self._slabs = [PinnedSlabs() for _ in range(self.depth)]
         self._engines = {}
         if not os.path.exists(self.candidateErrorLog):       # :86-87
@@ -736,7 +737,7 @@ class DataProcessor:
 
         _stream(paths, run.timed_parse(self._parse),
                 run.timed_score(lambda pre, slot: self._score(pre, mode, slot)), emit, self.batch,
-                self.depth)
+                self.depth, ramp=self.ramp)
         return counts["ok"], counts["failed"]
 
     # ---- 22 scores / profile bins ---------------------------------------------------
@@ -801,7 +802,7 @@ class DataProcessor:
 
         _stream(paths, run.timed_parse(self._parse),
                 run.timed_score(lambda pre, slot: self._score(pre, "scores", slot)), emit,
-                self.batch, self.depth)
+                self.batch, self.depth, ramp=self.ramp)
         self._summary(len(paths), counts["ok"], counts["failed"], start, run=run)
 
     def processPHCXSeparately(self, directory, verbose, processSingleCandidate):

@@ -109,7 +109,7 @@ def load(name):
 def bates_inputs(d):
     """Arrays in the libpfe layout from a bates22 golden set."""
     superb = bool(d["superb"])
-    if "dmcurve" in d.files:  # compact sets store the reduced curves and the block length
+    if "dmcurve" in d:  # compact sets store the reduced curves and the block length
         curves, blen = d["dmcurve"], int(d["block_len"])
     else:
         blk = d["block0"] if superb else d["block1"]

@@ -94,7 +94,7 @@ for step in "$@"; do
       python3 tools/sq_summary.py $O/${T}_sql8dm/p1 $O/${T}_sql8dm/p2 > $O/${T}_sql8dm_summary.json ;;
     e2e)
       timeout -k 10 600 python -u tools/e2e_bench.py --mode stream --n 50000 --dir /tmp/pfe_e2e \
-        --depth ${E2E_DEPTH:-1,2} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;
+        --depth ${E2E_DEPTH:-1,2} ${E2E_OPT} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;
     golden_dump)
       timeout -k 10 300 python -u tools/golden_dump.py $O/${T}_golden_gpu.npz > $O/${T}_golden_dump.log 2>&1 \
         || fail golden_dump $O/${T}_golden_dump.log ;;
