@@ -294,10 +294,13 @@ class PinnedSlabs:
     """Pinned host buffers (pfe_host_alloc) reused across batches and grown on demand: the
     native packer writes each shape group's rows straight into them and libpfe DMAs them in
     place.  view(key, shape, dtype) -> a numpy view of the slab `key` (valid until the next
-    view of the same key)."""
+    view of the same key).  rows: the batch size; a slab is first sized for that many rows
+    of its shape (shape[0] is the row count), so the ramped first batches of a run do not
+    regrow it (a pinned free synchronises the device)."""
 
-    def __init__(self):
+    def __init__(self, rows=0):
         self._slabs = {}
+        self.rows = int(rows)
 
     def view(self, key, shape, dtype):
         from ._native import host_empty
@@ -307,7 +310,10 @@ class PinnedSlabs:
         need = max(1, int(np.prod(shape, dtype=np.int64)) * dt.itemsize)
         s = self._slabs.get(key)
         if s is None or s.nbytes < need:
-            s = host_empty((need + need // 4 + 4096,), np.uint8)
+            want = need
+            if shape and 0 < shape[0] < self.rows:
+                want = need // shape[0] * self.rows
+            s = host_empty((want + want // 4 + 4096,), np.uint8)
             self._slabs[key] = s
         return s[:need].view(dt)[: int(np.prod(shape, dtype=np.int64))].reshape(shape)
 
@@ -444,7 +450,7 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True):
+                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=False):
         self.debug = debugFlag
         self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
@@ -465,8 +471,11 @@ class DataProcessor:
         # gpu_depth batches are scored at once (processor._stream), each slot with its own
         # engine handle (stream + workspace) and pinned slabs
         self.depth = max(1, int(gpu_depth))
-        self.ramp = bool(ramp)  # ramped batch sizes at both ends of a streamed run (_cuts)
-        self._slabs = [PinnedSlabs() for _ in range(self.depth)]
+        # ramped batch sizes at both ends of a streamed run (_cuts); off by default: measured
+        # slower for the 22 scores (each pfe_bates22 call has a fixed ~45 ms latency, and the
+        # extra calls cost more than the shorter first parse saves; profiles/r04_e2e_*)
+        self.ramp = bool(ramp)
+        self._slabs = [PinnedSlabs(self.batch) for _ in range(self.depth)]
         self._engines = {}
         if not os.path.exists(self.candidateErrorLog):       # :86-87
             writers.append_text(self.candidateErrorLog, "")
