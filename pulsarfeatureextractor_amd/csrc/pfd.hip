@@ -767,7 +767,10 @@ __global__ __launch_bounds__(64) void k_pfd_dmprof(PfdArgs a) {
   pfd_finish<false>(a, c, T, buf, tmp, dl, sdb, bv, chs, ftmp, po, dm_ok, lane);
 }
 
-constexpr int PFD4_E = 8;  // fold elements per thread and load step of k_pfd_dmprof4 (126 VGPRs)
+#ifndef PFE_PFD4_E
+#define PFE_PFD4_E 8
+#endif
+constexpr int PFD4_E = PFE_PFD4_E;  // fold elements per thread and load step of k_pfd_dmprof4
 
 // the accumulated sub-band rotations of the 100 trial DMs (PFDFile.py:395-416), one lane
 // per sub-band: rot[k][j] (the sweep of the single-wave kernel keeps them in cum / sdb)

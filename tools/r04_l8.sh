@@ -1,6 +1,10 @@
-# round 4 (temporary driver): PFD occupancy change, e2e ramp A/B, final suite, smoke, bench
+# round 4 (temporary driver): PFD part-reduction width A/B (E = 8 vs 12), pfd22 bench
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=r04 bash tools/gpu_steps.sh pytest:tests/test_pfd_gpu.py pytest:tests/test_pfd22_gpu.py pfdab && \
-TAG=r04nr E2E_OPT=--no-ramp bash tools/gpu_steps.sh e2e && \
-TAG=r04 bash tools/gpu_steps.sh e2e suite smoke bench
+for r in 1 2; do
+  for v in "" e12; do
+    PFE_LIBRARY=pulsarfeatureextractor_amd/lib/libpfe${v:+_$v}.so timeout -k 10 300 python3 bench.py --path pfd \
+      --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r04_pfd_e${v:-8}_$r.json 2> gpurun_out/r04_pfd_e.err || exit 1
+  done
+done
+timeout -k 10 600 python3 bench.py --path pfd22 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r04_pfd22.json 2> gpurun_out/r04_pfd22.err
