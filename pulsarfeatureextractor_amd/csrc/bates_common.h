@@ -97,7 +97,10 @@ constexpr int GDG8_FPW = 48;
 // fit slots per wave of the 4-parameter pooled kernels k_gt1g / k_gdgg up to 128 bins (two
 // waves per SIMD: BlmState<4, 44> + slot table + peel rows = 19 KB, 8 waves = 153 KB of LDS
 // per CU; their SIMT phase also runs one slot per lane)
-constexpr int GLM4_FPW = 44;
+#ifndef PFE_GLM4_FPW
+#define PFE_GLM4_FPW 44
+#endif
+constexpr int GLM4_FPW = PFE_GLM4_FPW;
 // work queues of the pooled kernels (BatesArgs::counters)
 constexpr int CTR_GT1G = 1, CTR_GDGG = 2, CTR_GDG8G = 3, CTR_DMG = 4, CTR_SINEG = 5, CTR_PFDDMG = 6,
               CTR_GHISTG = 7, CTR_GFIXG = 8, CTR_WIDE = 9, CTR_WIDEQ = 10;

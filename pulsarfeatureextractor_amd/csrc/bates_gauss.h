@@ -2063,7 +2063,13 @@ struct Gt1Prob {
 };
 
 template <int P>
-__global__ __launch_bounds__(64, 2) void k_gt1g(BatesArgs a) {
+#ifndef PFE_GT1G_WPE
+#define PFE_GT1G_WPE 2
+#endif
+#ifndef PFE_GDGG_WPE
+#define PFE_GDGG_WPE 2
+#endif
+__global__ __launch_bounds__(64, PFE_GT1G_WPE) void k_gt1g(BatesArgs a) {
   constexpr int FPW = P <= 2 ? GLM4_FPW : GLM_FPW;  // LDS: 256-bin peel rows keep 32
   constexpr int G = glm_group_lanes(64 * P);
   __shared__ BlmState<4, FPW> S;
@@ -2183,7 +2189,7 @@ struct PeelProb {
 };
 
 template <int P>
-__global__ __launch_bounds__(64, 2) void k_gdgg(BatesArgs a) {
+__global__ __launch_bounds__(64, PFE_GDGG_WPE) void k_gdgg(BatesArgs a) {
   constexpr int FPW = P <= 2 ? GLM4_FPW : GLM_FPW;  // LDS: 256-bin peel rows keep 32
   __shared__ BlmState<4, FPW> S;
   __shared__ SlotTab<FPW> T;
