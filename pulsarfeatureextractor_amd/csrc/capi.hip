@@ -57,6 +57,7 @@ struct pfe_handle {
   hipEvent_t ev_in[PIPE_SLOTS] = {}, ev_k[PIPE_SLOTS] = {}, ev_out[PIPE_SLOTS] = {};
   void* pin = nullptr;
   size_t pin_bytes = 0;
+  size_t scratch_bytes_peak = 0;  // the largest scratch allocated (growth policy)
   // split PFD pipeline (pfe_pfd_dmprof): two events per part-sum buffer, made on first use
   hipEvent_t pev[4] = {};
   std::string err;
@@ -107,8 +108,14 @@ static int ensure_scratch(pfe_handle* h, size_t bytes) {
     h->scratch = nullptr;
     h->scratch_bytes = 0;
   }
+  // grow by at least 4x below 1 GiB: a run whose batches grow (a ramped start) reallocates
+  // (device-wide synchronising free) once or twice, not at every size
+  const size_t old = h->scratch_bytes_peak;
   size_t want = bytes + (bytes >> 3) + 4096;
+  const size_t geo = old * 4 < ((size_t)1 << 30) ? old * 4 : ((size_t)1 << 30);
+  if (geo > want) want = geo;
   PFE_HIP(h, hipMalloc(&h->scratch, want));
+  h->scratch_bytes_peak = want;
   h->scratch_bytes = want;
   return PFE_OK;
 }

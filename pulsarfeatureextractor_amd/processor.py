@@ -450,7 +450,7 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=False):
+                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True):
         self.debug = debugFlag
         self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
@@ -471,9 +471,10 @@ class DataProcessor:
         # gpu_depth batches are scored at once (processor._stream), each slot with its own
         # engine handle (stream + workspace) and pinned slabs
         self.depth = max(1, int(gpu_depth))
-        # ramped batch sizes at both ends of a streamed run (_cuts); off by default: measured
-        # slower for the 22 scores (each pfe_bates22 call has a fixed ~45 ms latency, and the
-        # extra calls cost more than the shorter first parse saves; profiles/r04_e2e_*)
+        # ramped batch sizes at both ends of a streamed run (_cuts): the first GPU step starts
+        # after a short parse, the last one trails the last parse by little; with the slabs
+        # sized for the batch and the handle's workspace grown geometrically, faster in every
+        # alternating pair measured (profiles/r04_ab_e2e_ramp.txt)
         self.ramp = bool(ramp)
         self._slabs = [PinnedSlabs(self.batch) for _ in range(self.depth)]
         self._engines = {}

@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--mode", choices=["phases", "stream"], default="phases")
     ap.add_argument("--batch", type=int, default=8192)
-    ap.add_argument("--no-ramp", action="store_true", help="plain batches (no ramped ends)")
+    ap.add_argument("--ramp", type=int, default=1, help="ramped batch sizes at both ends (1, default) or not (0)")
     ap.add_argument("--depth", default="2",
                     help="GPU pipeline depths to time, comma-separated (DataProcessor gpu_depth)")
     args = ap.parse_args()
@@ -96,7 +96,7 @@ def main():
                 out = os.path.join(tempfile.mkdtemp(), "scores.csv")
                 dp = processor.DataProcessor(engine=eng, workers=args.workers,
                                              log=lambda *a: None, batch=args.batch,
-                                             gpu_depth=depth, ramp=not args.no_ramp)
+                                             gpu_depth=depth, ramp=bool(args.ramp))
                 t0 = time.perf_counter()
                 if kind == "scores":
                     dp.processPHCXCollectively(args.dir, False, out, False, False, False)
