@@ -631,8 +631,8 @@ def dm_kernel_name(ld):
     lv = leaves(ld - 8192 * (nch - 1))
     perfect = (len({d for _, d in lv}) == 1 and len(lv) <= 64 and
                all(64 <= m <= 128 and m % 8 == 0 for m, _ in lv))
-    if ld % 16 == 0 and nch <= 4 and perfect:  # fp64 moments up to two chunks (PFE_OPT_LYON8_DM 0)
-        return f"pfe::lyon8_u8_dm<{nch}, {'true' if nch <= 2 else 'false'}>"
+    if ld % 16 == 0 and nch <= 4 and perfect:  # fp64 moments (PFE_OPT_LYON8_DM 0)
+        return f"pfe::lyon8_u8_dm<{nch}, true>"
     return "pfe::lyon8_u8_long / lyon8_u8_generic"
 
 

@@ -115,11 +115,10 @@ int pfe_synchronize(pfe_handle* h);
  *                        (default 2)
  *   PFE_OPT_PFD_WAVES    waves per fold of the PFD preprocessing kernel: 4 (default) or 1
  *   PFE_OPT_LYON8_DM     Lyon-8 kernel for DataBlock-length DM rows (PHCX nDM x 128 bytes):
- *                        0 = lyon8_u8_dm, skew / kurt from fp64 d^3 / d^4 sums for rows of up
- *                        to two numpy chunks (nDM <= 128) and from exact integer power sums
- *                        beyond (default); 1 = the round-3 kernels; 2 = lyon8_u8_dm with the
- *                        exact power sums at every length.  Mean and std are numpy's bits with
- *                        every option; skew / kurt may differ in the last bits
+ *                        0 = lyon8_u8_dm, skew / kurt from fp64 d^3 / d^4 sums (default);
+ *                        1 = the round-3 kernels; 2 = lyon8_u8_dm with exact integer power
+ *                        sums.  Mean and std are numpy's bits with every option; skew / kurt
+ *                        may differ in the last bits
  *   PFE_OPT_PFD_SPLIT    PFD preprocessing: 1 = the folds' part sums streamed by their own kernel
  *                        on a side stream while the sweep kernel works on the previous chunk,
  *                        0 = one fused kernel (default; same bits)

@@ -853,14 +853,17 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
   }
 }
 
-// FPM (the default up to two chunks): skew / kurt from fp64 d^3 / d^4 sums fused into the
-// byte loop (2 fp64 FMAs per byte) instead of the exact integer power sums (3 packed integer
-// ops per byte).  Both run at half the VALU rate on gfx950 (profiles/r04_ubench_op_rates.txt:
-// ~5.1 and ~4.4 cycles per wave-instruction per SIMD), and the fp64 form frees the registers
-// of the 16-bit unpacking: 4.20 vs 4.47 ms per 1M rows at nDM = 120.  Beyond two chunks the
-// FPM form is not instantiated (the exact form needs no extra registers there).
+// FPM (the default): skew / kurt from fp64 d^3 / d^4 sums fused into the byte loop (2 fp64
+// FMAs per byte) instead of the exact integer power sums (3 packed integer ops per byte).
+// Both run at half the VALU rate on gfx950 (profiles/r04_ubench_op_rates.txt: ~5.1 and ~4.4
+// cycles per wave-instruction per SIMD), and the fp64 form frees the registers of the 16-bit
+// unpacking: 4.20 vs 4.47 ms per 1M rows at nDM = 120, and 6.40 vs 7.01 ms at nDM = 160 with
+// the 3- and 4-chunk forms at 3 waves per SIMD (profiles/r04_ab_dm_long.txt).
+#ifndef PFE_DM_WPE_LONG
+#define PFE_DM_WPE_LONG 3  // waves per SIMD of the 3- and 4-chunk forms (nDM > 128)
+#endif
 template <int NCH, bool FPM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : 2, NCH <= 2 ? 4 : 2)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : PFE_DM_WPE_LONG, NCH <= 2 ? 4 : PFE_DM_WPE_LONG)))
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
@@ -1187,6 +1190,10 @@ static int resident_blocks() {
   return cached[dev];
 }
 
+// rows of up to PFE_DM_FPM_MAXCH numpy chunks take the fp64-moment form by default
+#ifndef PFE_DM_FPM_MAXCH
+#define PFE_DM_FPM_MAXCH 4
+#endif
 template <int NCH, bool FPM>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
@@ -1210,15 +1217,18 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
   if (o.lyon8_dm != 1 && aligned && (lp == 64 || lp == 128 || lp == 256) && ld != 8192 &&
       ld != 16384 && dm_shape(lp, ld, dsh, dnch)) {
     // DataBlock rows (PHCX nDM x 128 bytes) other than the 2^k lengths: lyon8_u8_dm (DESIGN
-    // §3.1c), skew / kurt from fp64 d^3 / d^4 sums for rows of one or two numpy chunks (nDM <=
-    // 128, the faster of the two measured there), from the exact power sums beyond and with
-    // option 2 everywhere
+    // §3.1c), skew / kurt from fp64 d^3 / d^4 sums (the faster form at every length
+    // measured), from the exact power sums with option 2
     const int cap = o.lyon8_blocks;
-    if (o.lyon8_dm == 0 && dnch <= 2) {
-      if (dnch == 1)
-        launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
-      else
-        launch_dm_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap);
+    if (o.lyon8_dm == 0 && dnch <= PFE_DM_FPM_MAXCH) {
+      switch (dnch) {
+        case 1: launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+        case 2: launch_dm_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+#if PFE_DM_FPM_MAXCH > 2
+        case 3: launch_dm_kernel<3, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+        default: launch_dm_kernel<4, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+#endif
+      }
     } else {
       switch (dnch) {
         case 1: launch_dm_kernel<1, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
