@@ -100,10 +100,10 @@ def test_large_batch_properties(engine):
 def test_long_dm_rows_vs_oracle(engine, lp, ld):
     """The real PHCX shape: a 64-256-bin profile and the whole section-0 DataBlock (nDM x
     128 bytes; nDM = 120, 128, 60, 64, 100, 65, 3, 80, 112, 104, 96).  Kernels: nDM = 64 / 128
-    lyon8_u8_pow2 (exact leaf sums); 8192 + 2^j * {80, 96, 112, 128} bytes (nDM = 65, 80, 96,
-    104, 112, 120) lyon8_u8_lds; the rest lyon8_u8_long.  mean and std
-    bit-exact for both rows -- the DM row's std follows numpy's own reduction (8192-element
-    chunks, each a pairwise tree) -- skew/kurt within 1e-12."""
+    lyon8_u8_pow2 (exact leaf sums); every other length here lyon8_u8_dm (one wave per row,
+    numpy's chains byte by byte).  mean and std bit-exact for both rows -- the DM row's std
+    follows numpy's own reduction (8192-element chunks, each a pairwise tree) -- skew/kurt
+    within 1e-12."""
     prof, dm = lyon_batch(300, lp, ld, seed=31 + ld, adversarial=True)
     got = engine.lyon8(prof, dm)
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
