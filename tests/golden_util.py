@@ -127,7 +127,11 @@ def bates_inputs(d):
     return d["prof"], d["sub"], curves, scal
 
 
-_PERTS = (None, 1, -1, 2, -2, 4, "r7", "r11")
+# the unperturbed pass, the seven nudges, and the unperturbed pass once more: numpy's SIMD
+# reductions follow the heap alignment of their operands, so a second run (later in the
+# process, or in another spawned one) is a sample of the reference's own spread too (a row
+# whose fit changes basin between the two is not "stable")
+_PERTS = (None, 1, -1, 2, -2, 4, "r7", "r11", None)
 
 
 def _oracle_run(args):
@@ -155,10 +159,10 @@ def _oracle_run(args):
 
 def oracle_with_floor(prof, sub, curve, scal, workers=1):
     """Oracle scores of a fresh batch plus that batch's own chaos data (tools/chaos_rows.py,
-    applied to this batch): every leastsq start point nudged by +-1, +-2 and +4 ulp, and two
-    patterns of +-1 ulp on the residuals.  Returns (scores, status, floor, rmax): floor = the
+    applied to this batch): every leastsq start point nudged by +-1, +-2 and +4 ulp, two
+    patterns of +-1 ulp on the residuals, and a second unperturbed pass in another heap state.  Returns (scores, status, floor, rmax): floor = the
     fraction of candidates whose score moves by > 1e-5 / > 1e-3 relative under any of them,
-    rmax (n, 22) = each candidate's largest relative move.  workers > 1: the eight passes run
+    rmax (n, 22) = each candidate's largest relative move.  workers > 1: the nine passes run
     in spawned processes (no state is copied from a parent that holds a GPU context)."""
     tools = os.path.join(os.path.dirname(GOLDEN), "..", "tools")
     if tools not in sys.path:
