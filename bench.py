@@ -542,7 +542,7 @@ def run_subband(ctx, args, n, lsb, steps, warmup):
             "kernel": f"pfe::k_subband_fast<{lsb}, 4>",
             "algorithmic_bytes_per_candidate": per_cand,
             "note": "bytes-based roofline for comparability; the kernel is VALU-issue bound "
-                    "(about 2.2k wave instructions per candidate, 3 waves/SIMD at 159 VGPRs), "
+                    "(1.88k VALU wave instructions per candidate measured, profiles/r04_subband_sq_counters.json; 3 waves/SIMD at 166 VGPRs), "
                     "see DESIGN.md section 3.3",
             "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
         },

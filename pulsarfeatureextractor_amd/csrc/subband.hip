@@ -610,7 +610,9 @@ void k_subband_fast(SubArgs a) {
         kmax = kk > kmax ? kk : kmax;
         bv[ii][k] = b;
         sv += b;
-        qv += __umul24((uint32_t)b, (uint32_t)b);  // b < 2^16: the 24-bit multiply is exact
+        // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int, so
+        // the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
+        qv += (uint32_t)__umul24((uint32_t)b, (uint32_t)b);
       }
       sA[ii] = sv;
       qA[ii] = qv;

@@ -85,6 +85,22 @@ def test_subband3_vs_oracle(engine, nsub, lsb, n):
     check(out, st, ref, ok, f"{nsub}x{lsb}", lsb)
 
 
+@pytest.mark.parametrize("nsub,lsb", [(16, 64), (16, 128), (16, 256), (24, 200), (8, 512)])
+def test_subband3_bright_wide_windows(engine, nsub, lsb):
+    """Boxcar sums past 46 341 (b^2 >= 2^31): bright bands (bytes 180-255) and windows of
+    70-100 % of the band, so every sum of squares sits in the top bit of 32 bits or beyond."""
+    n = 24
+    b = bates_batch(n, lp=lsb, nsub=nsub, lsb=lsb, seed=900 + lsb)
+    rng = np.random.default_rng(lsb)
+    b["sub"][:] = rng.integers(180, 256, size=b["sub"].shape, dtype=np.uint8)
+    b["sub"][:, :, : lsb // 4] = 255
+    b["scal"][:, 3] = rng.uniform(0.7, 0.98, size=n)
+    out, st = engine.subband3(b["prof"], b["sub"], b["scal"])
+    ref, ok = oracle_sub(b["prof"], b["sub"], b["scal"])
+    assert ok.all()
+    check(out, st, ref, ok, f"bright {nsub}x{lsb}", lsb)
+
+
 def test_subband3_matches_bates22_columns_and_device(engine):
     import torch
 

@@ -17,6 +17,8 @@
 #   trace_l8dm   kernel trace of the nDM = 120 Lyon-8 kernel (tools/lyon8_long_bench.py)
 #   pmc_l8dm     FETCH_SIZE / WRITE_SIZE passes of the nDM = 120 command
 #   sq_l8dm      two SQ counter passes over the nDM = 120 kernel + tools/sq_summary.py
+#   sq_sub       two SQ counter passes over the config-4 sub-band kernel (bench.py --path subband)
+#   trace_sub    kernel trace of bench.py --path subband
 #   e2e          tools/e2e_bench.py --mode stream on 50 000 synthetic PHCX files
 #   golden_dump  the 22 scores of every golden set (tools/golden_dump.py; host: envelope_report)
 #   pfdab        bench.py --path pfd with the split pipeline (default) and fused (pfd_split=0)
@@ -92,6 +94,21 @@ for step in "$@"; do
           > $O/${T}_sql8dm_p$i.log 2>&1 || fail sq_l8dm $O/${T}_sql8dm_p$i.log
       done
       python3 tools/sq_summary.py $O/${T}_sql8dm/p1 $O/${T}_sql8dm/p2 > $O/${T}_sql8dm_summary.json ;;
+    sq_sub)
+      P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY"
+      P2="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT"
+      i=0
+      for p in "$P1" "$P2"; do
+        i=$((i + 1))
+        timeout -s KILL 180 rocprofv3 --pmc $p --output-format csv -d $O/${T}_sqsub/p$i -o pmc -- \
+          python3 bench.py --path subband --steps 2 --warmup 1 --no-cpu-baseline --no-extra \
+          > $O/${T}_sqsub_p$i.log 2>&1 || fail sq_sub $O/${T}_sqsub_p$i.log
+      done
+      python3 tools/sq_summary.py $O/${T}_sqsub/p1 $O/${T}_sqsub/p2 > $O/${T}_sqsub_summary.json ;;
+    trace_sub)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_trsub -o tr -- \
+        python3 bench.py --path subband --steps 10 --warmup 2 --no-cpu-baseline --no-extra \
+        > $O/${T}_trsub.json 2> $O/${T}_trsub.err || fail trace_sub $O/${T}_trsub.err ;;
     e2e)
       timeout -k 10 600 python -u tools/e2e_bench.py --mode stream --n 50000 --dir /tmp/pfe_e2e \
         --depth ${E2E_DEPTH:-1,2} ${E2E_OPT} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;
