@@ -19,17 +19,55 @@ namespace pfe {
 // ======================================================================================
 // scores 1-4
 // ======================================================================================
+// sin(c * x_k + phi) over a lane's rows x_k = x_0 + STRIDE k (STRIDE a power of two).
+// The residual models evaluate these at every function evaluation of the sine fits, and a
+// library sin is ~80-150 VALU instructions (its large-argument branch is if-converted).
+// Rows are walked by angle addition instead: one sincos at the anchor row (the reference's
+// own argument fl(fl(c x_0) + phi)), one of the exact step STRIDE * c, then per row
+//   s' = s C + c S,  c' = c C - s S                       (4 fp64 operations)
+// re-anchored every R rows.  Each rotation adds ~1 ulp, so a row's value differs from the
+// library sin of the reference's rounded argument by a few ulp of 1 -- the same order as
+// that argument's own rounding (ulp(c x_k)) once |c x_k| > 4, and the class of residual
+// perturbation the golden envelopes sample (tests/golden_util.py).  -DPFE_SIN_DIRECT builds
+// the per-row library sin for A/B.
+template <int M, int STRIDE, int R = 8>
+__device__ __forceinline__ void sin_rows(double c, double phi, const double (&x)[M],
+                                         double (&s)[M]) {
+#ifdef PFE_SIN_DIRECT
+#pragma unroll
+  for (int k = 0; k < M; ++k) s[k] = sin(c * x[k] + phi);
+#else
+  static_assert((STRIDE & (STRIDE - 1)) == 0, "an exact step needs a power-of-two stride");
+  double sd, cd;
+  sincos(c * (double)STRIDE, &sd, &cd);
+  double sk = 0.0, ck = 1.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    if (k % R == 0) {
+      sincos(c * x[k] + phi, &sk, &ck);
+    } else {
+      const double ns = fma(sk, cd, ck * sd);
+      const double nc = fma(ck, cd, -(sk * sd));
+      sk = ns;
+      ck = nc;
+    }
+    s[k] = sk;
+  }
+#endif
+}
+
 template <int MPL, bool SQR>
 struct SineFn {
   double x[MPL], y[MPL];
   bool ok[MPL];
   double amp, bg;
   __device__ __forceinline__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
-    const double c = TWO_PI * p[0];
+    double sv[MPL];
+    sin_rows<MPL, 64>(TWO_PI * p[0], p[1], x, sv);
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
       if (ok[k]) {
-        const double s = sin(c * x[k] + p[1]);
+        const double s = sv[k];
         if constexpr (!SQR)
           f[k] = y[k] - (fabs(amp) * s + fabs(bg));               // :418
         else
@@ -255,18 +293,19 @@ __global__ __launch_bounds__(BLOCK) void k_sine(BatesArgs a) {
 }
 
 // pooled group-LM form (lm_group.h): a slot runs a candidate's sine fit, then its sine^2 fit
-template <int MPL>
-struct SineAnyFn {  // SineFn<MPL, sqr> with the model chosen per slot
+template <int MPL, int STRIDE>
+struct SineAnyFn {  // SineFn<MPL, sqr> with the model chosen per slot (rows gl + STRIDE k)
   double x[MPL], y[MPL];
   bool ok[MPL];
   double amp, bg;
   bool sqr;
   __device__ __forceinline__ void operator()(const double (&p)[2], double (&f)[MPL]) const {
-    const double c = TWO_PI * p[0];
+    double sv[MPL];
+    sin_rows<MPL, STRIDE>(TWO_PI * p[0], p[1], x, sv);
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
       if (ok[k]) {
-        const double s = sin(c * x[k] + p[1]);
+        const double s = sv[k];
         f[k] = sqr ? (y[k] - (fabs(amp) * (s * s))) + fabs(bg)   // :522 (sign bug kept)
                    : y[k] - (fabs(amp) * s + fabs(bg));          // :418
       } else {
@@ -350,8 +389,8 @@ struct SineProb {
     blm_sync();
     return false;
   }
-  __device__ __forceinline__ SineAnyFn<MG> load(int f) const {
-    SineAnyFn<MG> fn;
+  __device__ __forceinline__ SineAnyFn<MG, G> load(int f) const {
+    SineAnyFn<MG, G> fn;
     const int64_t c = T.cand[f];
     const int lp = a.lp, gl = glane<G>();
 #pragma unroll
