@@ -21,6 +21,11 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 constexpr uint32_t ST_DEFER_HIST = 0x10000u;  // histogram has more bins than the kernel's slots
 constexpr uint32_t ST_DEFER_HIST64 = 0x20000u;  // > 64 bins: the pooled histogram kernels pass it on
 constexpr uint32_t ST_DEFER_WIDE = 0x40000u;    // > 1024 bins: queued for k_ghist_wide
+constexpr uint32_t ST_GAUSS_UNSUP = 0x80000u;   // the histogram group's own PFE_ST_UNSUPPORTED
+// failure bits the Gaussian chain skips a candidate on: only bits the chain sets itself, so
+// its work (and every output bit, failed rows included) never depends on how far the
+// concurrently running sine / DM / sub-band groups have got
+constexpr uint32_t GAUSS_SKIP = PFE_ST_GAUSS_FAIL | ST_GAUSS_UNSUP;
 // widest Freedman-Diaconis histogram scored (k_ghist_wide; rows in global scratch): the
 // uint8 profiles of <= 256 bins need at most ~10k (range 510 over an IQR of 1/4)
 constexpr int WIDE_MAX_BINS = 16384;

@@ -532,7 +532,7 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(BatesArgs a) {
     if (!BIG)
       st = ST_DEFER_HIST;
     else if (hb > WIDE_MAX_BINS || db > WIDE_MAX_BINS)
-      st = PFE_ST_UNSUPPORTED;
+      st = PFE_ST_UNSUPPORTED | ST_GAUSS_UNSUP;
     else {  // queue for k_ghist_wide (rows in global scratch)
       st = ST_DEFER_WIDE;
       if (lane == 0) a.wide_list[atomicAdd(a.counters + CTR_WIDE, 1u)] = (int)c;
@@ -1173,8 +1173,8 @@ struct GaussBgFn {  // y - (|A| exp(-((x-mu)/|sigma|)^2/2) + bg)      (:1226)
       }
     });
   }
-  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double (&f)[MPL],
-                                           const Cache& c) const {
+  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double,
+                                           double (&f)[MPL], const Cache& c) const {
     if (j < 2) {
       with_div(fabs(p[0]), p[1], [&](const auto& dv) {
 #pragma unroll
@@ -1267,7 +1267,7 @@ template <int P>
 __global__ __launch_bounds__(BLOCK) void k_gt1(BatesArgs a) {
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST)) return;
   const GaussWS w = a.ws[c];
   GaussBgFn<P> fn;
   gt1_setup<P>(a, c, w, fn);
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(64) void k_gt1b(BatesArgs a) {
   const int64_t base = (int64_t)blockIdx.x * fpw;
   const int lane = lane_id();
   const bool live = lane < fpw && base + lane < a.n &&
-                    !(a.status[base + (lane < fpw ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
+                    !(a.status[base + (lane < fpw ? lane : 0)] & (GAUSS_SKIP | ST_DEFER_HIST));
   const uint64_t fits = __ballot(live);
   if (fits == 0) return;
   const Gt1Loader<P> load{a, base};
@@ -1356,8 +1356,8 @@ struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
       }
     });
   }
-  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double (&f)[MPL],
-                                           const Cache& c) const {
+  __device__ __forceinline__ void eval_col(const double (&p)[4], int j, double,
+                                           double (&f)[MPL], const Cache& c) const {
     if (j < 2) {
       with_div(p[0], p[1], [&](const auto& dv) {
 #pragma unroll
@@ -1422,8 +1422,8 @@ struct DoubleGaussFn {  // :1459-1460
 #pragma unroll
     for (int k = 0; k < MPL; ++k) f[k] = ok[k] ? y[k] - combine(p, c.e1[k], c.e2[k]) : 0.0;
   }
-  __device__ __forceinline__ void eval_col(const double (&p)[8], int j, double (&f)[MPL],
-                                           const Cache& c) const {
+  __device__ __forceinline__ void eval_col(const double (&p)[8], int j, double,
+                                           double (&f)[MPL], const Cache& c) const {
     double e[MPL];
     if (j == 0 || j == 1) {
       with_div(fabs(p[0]), p[1], [&](const auto& dv) {
@@ -1658,7 +1658,7 @@ __global__ __launch_bounds__(BLOCK) void k_gdg(BatesArgs a) {
   __shared__ double cx_all[BLOCK / 64][64 * P];
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) return;
+  if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST)) return;
   const int lane = lane_id();
   const int L = a.lp;
   double* ys = ys_all[threadIdx.x >> 6];
@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(64) void k_gdgb(BatesArgs a) {
     const int64_t base = (int64_t)b * fpw;
     // candidates of this batch that reach the double-Gaussian fit
     const bool live = lane < fpw && base + lane < a.n &&
-                      !(a.status[base + (lane < fpw ? lane : 0)] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST));
+                      !(a.status[base + (lane < fpw ? lane : 0)] & (GAUSS_SKIP | ST_DEFER_HIST));
     uint64_t fits = __ballot(live);
     // prologue: peak removal, pass-1 rows and start points
     for (uint64_t m = fits; m; m &= m - 1) {
@@ -1903,7 +1903,7 @@ template <int P>
 __global__ __launch_bounds__(BLOCK) void k_gdg8(BatesArgs a) {
   const int64_t c = wave_candidate();
   if (c >= a.n) return;
-  if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) return;
+  if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) return;
   const int lane = lane_id();
   const int L = a.lp;
   const int cut = L / 2;
@@ -1962,7 +1962,7 @@ __global__ __launch_bounds__(64) void k_gdg8b(BatesArgs a) {
   bool part = false;
   if (lane < a.fpw) {
     const int64_t c = base + lane;
-    if (c < a.n && !(a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR))) {
+    if (c < a.n && !(a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR))) {
       part = true;
       const GaussWS* w = a.ws + c;
 #pragma unroll
@@ -2016,7 +2016,7 @@ struct Gt1Prob {
       for (;;) {
         const int64_t c = queue_next(a.counters + CTR_GT1G);
         if (c >= a.n) break;
-        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) continue;
+        if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST)) continue;
         GaussBgFn<P> fn;
         gt1_setup<P>(a, c, a.ws[c], fn);
         double p[4];
@@ -2137,7 +2137,7 @@ struct PeelProb {
       for (;;) {
         const int64_t c = queue_next(a.counters + CTR_GDGG);
         if (c >= a.n) break;
-        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST)) continue;
+        if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST)) continue;
         double y[P];
         bool ok[P];
         const int m1 = gdg_peel<P>(a, c, ys, cx, y, ok);
@@ -2232,7 +2232,7 @@ struct Gdg8Prob {
       for (;;) {
         const int64_t c = queue_next(a.counters + CTR_GDG8G);
         if (c >= a.n) break;
-        if (a.status[c] & (PFE_ST_FAIL_MASK | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) continue;
+        if (a.status[c] & (GAUSS_SKIP | ST_DEFER_HIST | PFE_ST_DGF_INDEXERROR)) continue;
         if (lane < 8) S.x[lane][f] = a.ws[c].dg[lane];
         if (lane == 0) T.cand[f] = c;
         blm_sync();

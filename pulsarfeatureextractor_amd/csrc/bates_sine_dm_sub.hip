@@ -456,8 +456,8 @@ struct DMFn {
       f[k] = ok[k] ? y[k] - p[0] * c.s[k] : 0.0;
     }
   }
-  __device__ __forceinline__ void eval_col(const double (&p)[3], int j, double (&f)[MPL],
-                                           const Cache& c) const {
+  __device__ __forceinline__ void eval_col(const double (&p)[3], int j, double,
+                                           double (&f)[MPL], const Cache& c) const {
 #pragma unroll
     for (int k = 0; k < MPL; ++k) {
       const double sh = (j == 0) ? c.s[k] : (ok[k] ? shape(p, k) : 0.0);

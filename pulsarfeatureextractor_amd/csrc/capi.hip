@@ -108,11 +108,14 @@ static int ensure_scratch(pfe_handle* h, size_t bytes) {
     h->scratch = nullptr;
     h->scratch_bytes = 0;
   }
-  // grow by at least 4x below 1 GiB: a run whose batches grow (a ramped start) reallocates
-  // (device-wide synchronising free) once or twice, not at every size
+  // grow geometrically (4x the previous peak, below 1 GiB): a run whose batches grow (a
+  // ramped start) reallocates (device-wide synchronising free) once or twice, not at every
+  // size -- but never beyond twice what this call asked for, so a handle does not keep
+  // several GiB for moderate batches
   const size_t old = h->scratch_bytes_peak;
   size_t want = bytes + (bytes >> 3) + 4096;
-  const size_t geo = old * 4 < ((size_t)1 << 30) ? old * 4 : ((size_t)1 << 30);
+  size_t geo = old * 4 < ((size_t)1 << 30) ? old * 4 : ((size_t)1 << 30);
+  if (geo > 2 * bytes) geo = 2 * bytes;
   if (geo > want) want = geo;
   PFE_HIP(h, hipMalloc(&h->scratch, want));
   h->scratch_bytes_peak = want;
@@ -637,7 +640,8 @@ int pfe_pfd_dmprof(pfe_handle* h, const pfe_pfd_in* in, double* profile, float* 
   a.n = n;
   a.waves = h->opt.pfd_waves;
   const size_t np = (size_t)n * in->npart * in->nsub * in->proflen;
-  // split pipeline: two buffers of part sums, chunks of up to 4096 folds (128 MB at 32 x 128)
+  // split pipeline: two buffers of part sums, chunks of up to 4096 folds
+  // (2 x 4096 x nsub x L doubles: 268 MB at 32 x 128)
   const bool split = h->opt.pfd_split && h->fork.side[0] && pfe::pfd_split_ok(a);
   const int64_t chunk = n < 4096 ? n : 4096;
   const size_t wsb = split ? align256(2 * (size_t)chunk * in->nsub * in->proflen * sizeof(double)) : 0;

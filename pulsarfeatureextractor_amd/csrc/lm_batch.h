@@ -65,11 +65,13 @@ __device__ __forceinline__ void fn_eval(const Fn& fn, const double (&p)[N], doub
   else
     fn(p, f);
 }
+// p = the base point with parameter j moved from pj0 to pj0 + h (the forward-difference
+// column j); pj0 lets a functor rebuild the base point's intermediate terms
 template <class Fn, int N, int MPL>
-__device__ __forceinline__ void fn_eval_col(const Fn& fn, const double (&p)[N], int j,
+__device__ __forceinline__ void fn_eval_col(const Fn& fn, const double (&p)[N], int j, double pj0,
                                             double (&f)[MPL], const typename FnCache<Fn>::type& c) {
   if constexpr (HasCols<Fn>::value)
-    fn.eval_col(p, j, f, c);
+    fn.eval_col(p, j, pj0, f, c);
   else
     fn(p, f);
 }
@@ -101,7 +103,7 @@ __device__ __forceinline__ void blm_outer(const Fn& fcn, const double (&fvec)[MP
     double h = eps * fabs(temp);
     if (h == 0.0) h = eps;
     x[j] = temp + h;
-    fn_eval_col<Fn, N, MPL>(fcn, x, j, wa4, cache);
+    fn_eval_col<Fn, N, MPL>(fcn, x, j, temp, wa4, cache);
     x[j] = temp;
     const double rh = 1.0 / h;
 #pragma unroll

@@ -100,7 +100,7 @@ __device__ __forceinline__ void gsum_from(double (&v)[K], int lo) {
 template <int J>
 __device__ __forceinline__ double nbc(double v) {
   return __longlong_as_double(
-      __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xF, 0xF, false));
+      __builtin_amdgcn_mov_dpp(__double_as_longlong(v), 0x150 + J, 0xF, 0xF, true));
 }
 __device__ __forceinline__ double gbcast16(double v, int j) {
   switch (j) {
@@ -312,6 +312,16 @@ struct HandOver {
   }
 };
 
+// Cost probes (timing builds only, never the product): -DPFE_DUP_EVAL evaluates every trial
+// point twice, -DPFE_DUP_COLS every Jacobian column twice, -DPFE_DUP_QR factors every
+// Jacobian twice (the copies' results are kept live and dropped), so the time each adds is
+// the cost of that part of the solver (tools/ab_lib_bates.sh)
+template <int M>
+__device__ __forceinline__ void probe_keep(const double (&a)[M]) {
+#pragma unroll
+  for (int k = 0; k < M; ++k) asm volatile("" ::"v"(a[k]));
+}
+
 // O-phase for slot f (one group): residuals at S.x (a fresh fit also initialises par, delta,
 // xnorm, the counters and fnorm), the forward-difference Jacobian, QR, Q^T f, R -> LDS.
 // Leaves info = -1 (the gtol test runs in the next SIMT phase).
@@ -348,7 +358,14 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
     double h = eps * fabs(temp);
     if (h == 0.0) h = eps;
     x[j] = temp + h;
-    fn_eval_col<Fn, N, MPL>(fcn, x, j, wa4, cache);
+#ifdef PFE_DUP_COLS
+    {
+      double w2[MPL];
+      fn_eval_col<Fn, N, MPL>(fcn, x, j, temp, w2, cache);
+      probe_keep(w2);
+    }
+#endif
+    fn_eval_col<Fn, N, MPL>(fcn, x, j, temp, wa4, cache);
     x[j] = temp;
     const double rh = 1.0 / h;
 #pragma unroll
@@ -357,6 +374,19 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   nfev += N;
   int ipvt[N];
   double rdiag[N], acn[N], rajjv[N];
+#ifdef PFE_DUP_QR
+  {
+    double a2[MPL][N], r2[N], c2[N], j2[N];
+    int p2[N];
+#pragma unroll
+    for (int k = 0; k < MPL; ++k)
+#pragma unroll
+      for (int j = 0; j < N; ++j) a2[k][j] = fjac[k][j];
+    qrfac_g<N, MPL, G>(a2, p2, r2, c2, j2);
+    probe_keep(r2);
+    probe_keep(j2);
+  }
+#endif
   qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn, rajjv);
   // the contracted build leaves acn squared and the scaling (diag, and xnorm / delta of a
   // fresh fit) to the next SIMT phase, one fit per lane (blm_simt<.., true>)
@@ -436,6 +466,14 @@ __device__ __forceinline__ int glm_trial(const Fn& fcn, int f, BlmState<N, FPW>&
   typename FnCache<Fn>::type cache;
 #pragma unroll
   for (int j = 0; j < N; ++j) wa2[j] = S.trial[j][f];
+#ifdef PFE_DUP_EVAL
+  {
+    double w2[MPL];
+    typename FnCache<Fn>::type c2;
+    fn_eval<Fn, N, MPL>(fcn, wa2, w2, c2);
+    probe_keep(w2);
+  }
+#endif
   fn_eval<Fn, N, MPL>(fcn, wa2, wa4, cache);
   const int nfev = S.nfev[f] + 1;
   const double fnorm1 = enorm_g<MPL, G>(wa4);

@@ -60,7 +60,11 @@ __device__ __noinline__ double np_pairwise<0>(const double* a, int n, int lane) 
   return np_leaf(a, n, lane);
 }
 
-// np_pairwise with every level inlined (no call): exact for n <= 128 * 2^D
+// np_pairwise with every level inlined (no call).  numpy splits at floor8(n/2), so the larger
+// half n - floor8(n/2) can exceed n/2 (969 -> 489 -> 249 -> 129): D levels reproduce numpy's
+// order exactly for n <= np_inl_max(D) = 128, 248, 488, 968, 1928 (D = 0..4), not 128 * 2^D
+__host__ __device__ constexpr int np_inl_max(int D) { return D == 0 ? 128 : 2 * (np_inl_max(D - 1) - 4); }
+static_assert(np_inl_max(1) == 248 && np_inl_max(3) == 968, "numpy pairwise split bound");
 template <int D>
 __device__ __forceinline__ double np_pairwise_inl(const double* a, int n, int lane) {
   if (n <= 128 || D == 0) return np_leaf(a, n, lane);

@@ -34,7 +34,7 @@ __device__ __forceinline__ double delay_from_dm(double dm, double f) {  // PFDOp
 
 // numpy's pairwise sum of an LDS row with the leaf's loads issued before its adds when the
 // row is a single leaf (np_leaf128: the same order of additions, so the same bits)
-// NC (the four-wave kernel, rows of <= 1024 values): every level inlined, no call -- a call
+// NC (the four-wave kernel, rows of <= np_inl_max(3) = 968 values): every level inlined, no call -- a call
 // in a kernel makes the backend assume the callee's register needs (212 VGPRs and 2 waves per
 // SIMD for k_pfd_dmprof4 with the recursive call in it, 123 without)
 template <bool NC = false>
@@ -1138,10 +1138,12 @@ static size_t pfd4_lds_bytes(int nsub, int L) {
          4 * 256 * sizeof(double);
 }
 
-// the four-wave kernel: <= 128 bins, the fold in LDS, and rows of <= 1024 values (its
+// the four-wave kernel: <= 128 bins, the fold in LDS, and rows of <= 968 values (its
 // pairwise sums are inlined three levels deep, np_sum_row<true>)
 static bool pfd4_ok(const PfdArgs& a) {
-  return a.L <= 128 && a.nsub <= 1024 && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 && a.waves == 4;
+  // nsub: the sub-band sums go through np_pairwise_inl<3>, numpy's order up to np_inl_max(3)
+  return a.L <= 128 && a.nsub <= np_inl_max(3) && pfd4_lds_bytes(a.nsub, a.L) <= 64 * 1024 &&
+         a.waves == 4;
 }
 
 bool pfd_split_ok(const PfdArgs& a) {

@@ -41,9 +41,14 @@ constexpr int DPP_QUAD_XOR2 = 0x4E;  // [2,3,0,1]
 constexpr int DPP_ROW_HALF_MIRROR = 0x141;  // lane i <-> 7-i within each 8-lane half-row
 constexpr int DPP_ROW_MIRROR = 0x140;       // lane i <-> 15-i within each 16-lane row
 
+// Full row / bank masks and bound_ctrl = 1: a lane whose source is outside its row (the
+// shift controls) reads 0, every other lane the selected source -- the result of
+// update_dpp(0, v, ..., bound_ctrl = 0), but with no `old` operand, so the compiler does not
+// materialise a zero into the destination before every v_mov_b32_dpp (two v_mov_b32 per
+// 64-bit step of every group reduction; the same bits)
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 
 template <int CTRL>

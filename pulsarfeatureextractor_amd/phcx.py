@@ -143,6 +143,44 @@ def parse(path: str, superb: bool | None = None) -> PHCXCandidate:
                          period_ms=period_ms, snr=snr, dm=dmv, width=width)
 
 
+def is_valid(path: str, superb: bool | None = None) -> bool:
+    """PHCXFile.isValid (PHCXFile.py:190-287) / SUPERBPHCXFile.isValid (SUPERBPHCXFile.py:
+    190-): the reference's well-formedness test of a candidate file, run only in debug (-v)
+    mode (PHCXFile.load :108-118).  False: the three block tags do not occur exactly twice,
+    the section-1 profile text is <= 100 characters or the sub-band / DataBlock texts
+    <= 1000, SubBands[1] is not nBins = 128 (64 for SUPERB) x nSub = 16, or the DmIndex[1]
+    text is <= 100 characters.  The NaN test (:250) compares floats with the string "nan"
+    and never fails, but its float() of Width / Snr / Dm / BaryPeriod[1] can raise, and so
+    can a missing element: those exceptions propagate as in the reference."""
+    if superb is None:
+        superb = ".gz" not in path
+    root = _read_xml(path, superb)
+
+    def elems(tag):
+        return list(root.iter(tag))
+
+    def text(el):  # minidom childNodes[0].data: IndexError for an empty element
+        if el.text is None:
+            raise IndexError("list index out of range")
+        return el.text
+
+    prof, sub, blk = elems("Profile"), elems("SubBands"), elems("DataBlock")
+    if not (len(prof) == len(sub) == len(blk) == 2):
+        return False
+    sub_fft, blk_fft = text(sub[0]), text(blk[0])  # noqa: F841 (read as the reference does)
+    prof_opt, sub_opt, blk_opt = text(prof[1]), text(sub[1]), text(blk[1])
+    if not (len(prof_opt) > 100 and len(sub_opt) > 1000 and len(sub_fft) > 1000 and
+            len(blk_opt) > 1000):
+        return False
+    nbins, nsub = int(sub[1].get("nBins")), int(sub[1].get("nSub"))
+    ndmi = len(text(elems("DmIndex")[1]))
+    if not (nbins == (64 if superb else 128) and nsub == 16 and ndmi > 100):
+        return False
+    for tag in ("Width", "Snr", "Dm", "BaryPeriod"):
+        float(text(elems(tag)[1]))
+    return True
+
+
 # ---------------------------------------------------------------------------------------
 # synthetic writer (fixtures, tests, CLI demos)
 # ---------------------------------------------------------------------------------------

@@ -25,6 +25,7 @@ import datetime
 import fnmatch
 import json
 import os
+import threading
 import time
 from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 
@@ -401,9 +402,12 @@ class RunMetrics:
         self.stage = {}  # finer host timers of the GPU stage (pack, gpu), summed over slots
         self.batches = 0
         self.reasons = {}
+        # the pipeline's slot threads add to the same timers concurrently
+        self._lock = threading.Lock()
 
     def add(self, key, dt):
-        self.stage[key] = self.stage.get(key, 0.0) + dt
+        with self._lock:
+            self.stage[key] = self.stage.get(key, 0.0) + dt
 
     def timed_parse(self, fn):
         def wrapped(paths):
@@ -420,7 +424,9 @@ class RunMetrics:
             try:
                 return fn(pre, slot)
             finally:
-                self.score_s += time.perf_counter() - t
+                dt = time.perf_counter() - t
+                with self._lock:
+                    self.score_s += dt
         return wrapped
 
     def batch(self, res):
@@ -452,6 +458,7 @@ class DataProcessor:
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
                  start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True):
         self.debug = debugFlag
+        self.verbose = False  # the entry point's verbose flag (-v): isValid per PHCX file
         self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
         self.metrics = None   # RunMetrics.as_dict() of the last mode run
@@ -556,12 +563,20 @@ class DataProcessor:
         time).  A non-libpfe engine (a test stub) serves every slot."""
         from ._native import Engine
 
+        from ._native import OPTIONS
+
         base = self.engine or get_engine()
         if slot == 0 or not isinstance(base, Engine):
             return base
         e = self._engines.get(slot)
         if e is None:
             e = self._engines[slot] = Engine(base.device)
+        # every handle option of the caller's engine (solver, kernels, pools ...), read again
+        # at each batch: the slots of one run compute exactly what the caller's engine would
+        for name in OPTIONS:
+            v = base.get_option(name)
+            if e.get_option(name) != v:
+                e.set_option(name, v)
         return e
 
     def _slab(self, slot):
@@ -708,7 +723,37 @@ class DataProcessor:
                 self._score_pfd(pre, mode, res, slot)
         finally:
             pre.close()
+        if self.verbose and len(pre.px):
+            self._debug_validity(pre, mode, res)
         return res
+
+    def _debug_validity(self, pre, mode, res):
+        """Debug (-v) mode: PHCXFile.load (PHCXFile.py:108-134) runs isValid on every PHCX /
+        SUPERB file first.  An invalid file keeps 22 NaN scores and an EMPTY profile list, so
+        compute()'s sine group then fails (profile.mean() of a list: "Sinusoid fitting
+        exception", :470) and the 22-score modes drop the file; the Lyon mode's profile
+        moments of [] are NaN (numpy mean / std of an empty list) while the DM-curve moments,
+        read from the XML, are unchanged.  An exception inside isValid fails the file.  The
+        reference's debug prints and matplotlib windows are not reproduced."""
+        for k in range(len(pre.px)):
+            i = int(pre.px[k])
+            if res.err[i]:
+                continue
+            path = pre.paths[i]
+            try:
+                valid = _phcx.is_valid(path)
+            except Exception as e:  # noqa: BLE001 -- the reference's load() raises it
+                res.err[i] = f"{type(e).__name__}: {e}"
+                continue
+            if valid:
+                continue
+            self.log(f"Invalid {'SUPERB ' if '.gz' not in path else ''}PHCX candidate:  {path}")
+            if mode in ("scores", "label"):
+                res.err[i] = GROUP_ERRORS[0][1]
+            elif mode == "lyon8":
+                res.mat[i, :4] = np.nan
+            else:  # profile mode: computeProfileScores of the empty profile
+                res.rows[i] = np.zeros(0)
 
     def _stream_text(self, paths, mode, out_path, style, run):
         """Collective modes: stream parse -> score, append each batch's lines (pfe_format_rows,
@@ -753,6 +798,7 @@ class DataProcessor:
     # ---- 22 scores / profile bins ---------------------------------------------------
     def processCollectively(self, directory, verbose, regexes, outPath, arff, genProfileData,
                             single):
+        self.verbose = bool(verbose)
         if arff and not self._resuming(outPath):              # prepareARFFFile (:329-367)
             nattr = 22
             if genProfileData and self.superb:
@@ -787,6 +833,7 @@ class DataProcessor:
 
     def processSeparately(self, directory, verbose, regexes, single):
         """:603-687 — each candidate's 22 scores into <candidate>.dat."""
+        self.verbose = bool(verbose)
         start = datetime.datetime.now()
         run = RunMetrics("separately", self.start)
         paths = self._candidates(directory, regexes, single)
@@ -821,6 +868,7 @@ class DataProcessor:
 
     # ---- 8 Lyon features -------------------------------------------------------------
     def dmprof(self, directory, verbose, regexes, outPath, arff, single):
+        self.verbose = bool(verbose)
         if arff and not self._resuming(outPath):
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
@@ -864,6 +912,7 @@ class DataProcessor:
         out (:754-774), so every label is "0" and the positive/negative counts stay 0.
         Values are written as the reference's Python-2 str() writes them (no nan/inf
         replacement here, unlike storeScore)."""
+        self.verbose = bool(verbose)
         if directory == "":
             directory = os.path.dirname(os.path.realpath(__file__))
         meta = directory + "/Cands.meta"
@@ -901,7 +950,7 @@ class DataProcessor:
 
         _stream(paths, run.timed_parse(self._parse),
                 run.timed_score(lambda pre, slot: self._score(pre, "label", slot)), emit,
-                self.batch, self.depth)
+                self.batch, self.depth, ramp=self.ramp)
         self._summary(len(paths), counts["ok"], counts["failed"], start,
                       f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n", run=run)
 

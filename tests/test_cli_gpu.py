@@ -138,3 +138,32 @@ def test_pfd_dmprof_and_profile_cli(tmp_path, monkeypatch):
     assert cli.main(["-c", str(cand), "-o", str(tmp_path / "absent" / "x.csv"), "--pfd"]) == 0
     dats = sorted(p for p in os.listdir(cand) if p.endswith(".dat"))
     assert len(dats) == int(g["bates22_ok"].sum())
+
+
+def test_pipeline_slots_follow_the_callers_engine_options(tmp_path, monkeypatch):
+    """gpu_depth = 2 scores odd batches on a second libpfe handle: every option set on the
+    engine the caller passed (solver, pool size, ...) must reach that handle too, so one output
+    file never mixes two configurations (round-4 advisor finding)."""
+    from pulsarfeatureextractor_amd import processor
+    from pulsarfeatureextractor_amd._native import OPTIONS, Engine
+
+    monkeypatch.chdir(tmp_path)
+    d = load("bates22_phcx128")
+    write_set(d, str(tmp_path / "cands"))
+    outs = {}
+    with Engine(0) as e:
+        e.set_option("solver", "batched")
+        e.set_option("gslots", 7)
+        for depth in (1, 2):
+            p = processor.DataProcessor(engine=e, batch=64, gpu_depth=depth, ramp=False,
+                                        log=lambda *a: None)
+            out = str(tmp_path / f"d{depth}.csv")
+            p.processPHCXCollectively(str(tmp_path / "cands"), False, out, False, False, False)
+            outs[depth] = open(out).read()
+            if depth == 2:
+                slot = p._eng(1)
+                assert slot is not e
+                for name in OPTIONS:
+                    assert slot.get_option(name) == e.get_option(name), name
+        # both slots computed with the batched solver: the same text as one slot
+        assert outs[1] == outs[2]

@@ -93,6 +93,52 @@ def test_large_batch_properties(engine):
     check(a[idx].cpu().numpy(), lyon8_batched(sp, sd))
 
 
+def test_config2_full_size_10m(engine):
+    """BASELINE config 2 at the size it names, on the benched rows themselves (bench.py's
+    generator and seed): one pfe_lyon8_u8 launch over 10M resident 128 + 128-byte candidates.
+      * mean and std of both rows (columns 0, 1, 4, 5) bit-exact on EVERY row: numpy's sums
+        of byte rows of 128 are exact, so x.sum() / 128 and sqrt(sum((x - mean)^2) / 128) are
+        correctly rounded functions of the exact sums -- computed here with torch in fp64;
+      * all 8 features of 2000 rows drawn from the last million against the oracle;
+      * a 16384-row block tiled to 10M rows (as bench.py's config-3 line tiles): every tile
+        bit-identical to the first (a grid-stride or 32-bit indexing fault past a few million
+        rows breaks that)."""
+    import torch
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    n = 10_000_000
+    tp, td = lyon_batch_torch(n, 128, 128, seed=20261017)   # bench.py's config-2 rows
+    out = engine.lyon8(tp, td)
+    engine.synchronize()
+    for rows, (cm, cs) in ((tp, (0, 1)), (td, (4, 5))):
+        for s in range(0, n, 1 << 20):
+            x = rows[s:s + (1 << 20)].to(torch.float64)
+            mean = x.sum(dim=1) / 128.0
+            std = torch.sqrt(((x - mean[:, None]) ** 2).sum(dim=1) / 128.0)
+            o = out[s:s + (1 << 20)]
+            assert torch.equal(o[:, cm], mean), f"mean, rows {s}.."
+            assert torch.equal(o[:, cs], std), f"std, rows {s}.."
+    idx = torch.randint(n - 1_000_000, n, (2000,), generator=torch.Generator().manual_seed(7))
+    check(out[idx].cpu().numpy(), lyon8_batched(tp[idx].cpu().numpy(), td[idx].cpu().numpy()))
+    del out, tp, td
+    blk = 16384
+    bp, bd = lyon_batch_torch(blk, 128, 128, seed=20261018)
+    reps = (n + blk - 1) // blk
+    tp = bp.repeat(reps, 1)[:n].contiguous()
+    td = bd.repeat(reps, 1)[:n].contiguous()
+    out = engine.lyon8(tp, td)
+    engine.synchronize()
+    ob = out.view(torch.int64)
+    full = (n // blk) * blk
+    tiles = ob[:full].view(-1, blk, 8)
+    bad = (tiles != tiles[:1]).any(dim=2).any(dim=1)
+    assert not bool(bad.any()), f"tiles differing from tile 0: {torch.nonzero(bad)[:10].flatten().tolist()}"
+    assert torch.equal(ob[full:], ob[: n - full])
+    check(out[:blk].cpu().numpy(), lyon8_batched(bp.cpu().numpy(), bd.cpu().numpy()))
+    del out, ob, tiles, tp, td
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("lp,ld", [(128, 15360), (128, 16384), (64, 7680), (256, 8192),
                                    (128, 12800), (128, 8320), (64, 384), (256, 10240),
                                    (64, 16384), (256, 16384), (128, 8192), (64, 8192),

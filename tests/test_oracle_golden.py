@@ -5,8 +5,10 @@ reference itself run on synthetic PHCX/SUPERB files -- are the pin.
 
 Bar:
   * Lyon-8: bit-exact (same numpy/scipy calls on the same rows).
-  * Bates-22: same failing candidates; bit-exact on every score outside class C (the LM
-    outputs s7-s11, s17, s18); those inside the reference's own 50-sample envelope, s10/s11
+  * Bates-22: same failing candidates; bit-exact on every score but s10/s11 on the original
+    sets, and outside class C (the LM outputs s7-s11, s17, s18) on the round-4 big sets, where
+    the class-C scores are bit-exact on the rows the reference's envelope calls tight; all
+    LM scores inside the reference's own 50-sample envelope, s10/s11
     also within 1e-5 relative of the golden draw in >= 70% of rows, the others in >= 90%.  The reference is not bit-reproducible against
     ITSELF on s10/s11: the same candidate scored twice in one process (different heap state)
     moves s10/s11 in 4-18% of rows (last-bit differences inside numpy/MINPACK that the
@@ -16,7 +18,8 @@ Bar:
 import numpy as np
 import pytest
 
-from golden_util import CLASS_C, SELF_NOISY, bates_inputs, envelope_check, load
+from golden_util import (CLASS_C, ENVELOPE_TIGHT, FIT_GROUPS, GOLDEN, SELF_NOISY, bates_inputs,
+                         envelope_check, load)
 from oracle.bates import bates22
 from oracle.lyon import lyon8
 
@@ -30,6 +33,23 @@ def test_lyon8_oracle_bit_exact(name):
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     m = ~np.isnan(ref)
     assert np.array_equal(got[m], ref[m])
+
+
+def envelope_tight(name):
+    """(n, 22) rows where the reference's 50 samples agree to ENVELOPE_TIGHT on a score and on
+    every other output of the same fit (golden_util.envelope_check's rule)."""
+    import os
+
+    env = np.load(os.path.join(GOLDEN, "chaos_envelope.npz"))
+    lo, hi = env[f"{name}_lo"], env[f"{name}_hi"]
+    with np.errstate(all="ignore"):
+        t = (hi - lo) <= ENVELOPE_TIGHT * np.maximum(np.abs(lo), np.abs(hi))
+    t |= np.isnan(lo) & np.isnan(hi)
+    for grp in FIT_GROUPS:
+        both = np.logical_and.reduce([t[:, j] for j in grp])
+        for j in grp:
+            t[:, j] = both
+    return t
 
 
 @pytest.mark.parametrize("name,rows", [("bates22_phcx128", 90), ("bates22_superb64", 45),
@@ -49,9 +69,18 @@ def test_bates22_oracle_vs_reference(name, rows):
     same = (got == ref) | (np.isnan(got) & np.isnan(ref))
     with np.errstate(all="ignore"):
         close = same | (np.abs(got - ref) <= 1e-5 * np.abs(ref))
+    # bit-exact: every score but s10/s11 on the original sets (round 1-3, made where the
+    # oracle reproduced the reference); on the 1000 / 500-row sets of round 4 the class-C fits
+    # only where the reference's own 50-sample envelope is tight -- a chaotic row of s7-s9,
+    # s17, s18 can land on another of the reference's values
+    big = name.endswith("_big")
+    tight = envelope_tight(name)[sel][m]
     for j in range(22):
-        if j not in CLASS_C:
-            assert same[:, j].all(), f"s{j + 1} not bit-exact in {(~same[:, j]).sum()} rows"
+        if j in SELF_NOISY:
+            continue
+        must = np.ones(len(got), dtype=bool) if (j not in CLASS_C or not big) else tight[:, j]
+        bad = must & ~same[:, j]
+        assert not bad.any(), f"s{j + 1} not bit-exact in {bad.sum()} rows"
     # the LM outputs (class C): the oracle's draw inside the reference's envelope (tight rows
     # all, chaotic rows to the binomial bound) -- on the larger sets a chaotic row can move
     # s8 or s17 between two runs of the oracle itself; the 70% single-draw agreement of

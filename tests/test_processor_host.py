@@ -234,3 +234,55 @@ def test_stream_cuts_ramp():
     assert sizes.max() == 8192
     assert _cuts(100, 8192) == [0, 100]
     assert _cuts(20, 8) == [0, 8, 16, 20]
+
+
+def test_verbose_runs_the_reference_validity_checks(tmp_path, monkeypatch):
+    """-v (debug): PHCXFile.load runs isValid (PHCXFile.py:190-287) on each file.  The golden
+    files are valid; a file with 64-bin sub-bands is not, and an invalid file leaves an empty
+    profile, so the 22-score modes fail it in the sine group while the Lyon mode writes NaN
+    profile moments (-> "0") and its unchanged DM-curve moments.  Without -v nothing changes."""
+    monkeypatch.chdir(tmp_path)
+    d = tmp_path / "cands"
+    d.mkdir()
+    good = _write_golden(str(d), "bates22_phcx128", range(6))
+    assert all(phcx.is_valid(p) for p in good)
+    c = phcx.parse(good[0])
+    bad = str(d / "zz_bad.phcx.gz")
+    phcx.write(bad, profile=c.profile, subbands=np.zeros((16, 64), np.uint8),
+               datablocks=(np.zeros(128 * 120, np.uint8), np.zeros(128 * 120, np.uint8)),
+               dm_start=0.0, dm_end=100.0, n_dm_index=120, period_s=0.5, snr=10.0, dm=12.0,
+               width=0.05)
+    assert not phcx.is_valid(bad)
+    # section 0's SubBands empty: scored normally (section 1 is read), but isValid's
+    # childNodes[0] of that element raises
+    with gzip.open(good[0], "rb") as f:
+        text = f.read().decode()
+    i = text.index("<SubBands")
+    i = text.index(">", i) + 1
+    broken = str(d / "zz_raise.phcx.gz")
+    with gzip.open(broken, "wb") as f:
+        f.write((text[:i] + text[text.index("</SubBands>", i):]).encode())
+    with pytest.raises(IndexError):
+        phcx.is_valid(broken)
+    assert len(phcx.parse(broken).profile) == 128
+    logs = []
+    for verbose in (False, True):
+        dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=logs.append, batch=4)
+        dp._slabs = PlainSlabs()
+        out = str(tmp_path / f"s{int(verbose)}.csv")
+        dp.processPHCXCollectively(str(d) + "/", verbose, out, False, False, False)
+        names = [ln.split(",")[0] for ln in open(out).read().splitlines()]
+        assert (bad in names) != verbose and (broken in names) != verbose
+        ok_good = [p for p, _v in expected(good, "bates22")[0]]
+        assert [g for g in good if g in names] == ok_good
+        dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=logs.append, batch=4)
+        dp._slabs = PlainSlabs()
+        out8 = str(tmp_path / f"l{int(verbose)}.csv")
+        dp.dmprofPHCX(str(d) + "/", verbose, out8, False, False)
+        rows = {ln.split(",")[0]: ln.split(",")[1:] for ln in open(out8).read().splitlines()}
+        assert (broken in rows) != verbose
+        if verbose:
+            assert rows[bad][:4] == ["0"] * 4 and rows[bad][4:] != ["0"] * 4
+        else:
+            assert rows[bad][:4] != ["0"] * 4
+    assert any("Invalid PHCX candidate" in str(m) for m in logs)
