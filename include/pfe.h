@@ -65,9 +65,9 @@ extern "C" {
                                         for byte (PHCX) profiles of up to 32768 bins: their
                                         non-zero IQR is a multiple of 0.25, so the bin count
                                         is at most 510 n^(1/3); or, in pfe_bates22, a
-                                        sub-band shape outside nsub 2-256, nBins 1-1024,
-                                        nsub*(nBins+1) <= 32768 -- the other groups' scores
-                                        are still computed).  The row is not scored */
+                                        sub-band shape beyond nsub 65536 x nBins 16384 --
+                                        the other groups' scores are still computed).  The
+                                        row is not scored */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu
@@ -213,9 +213,34 @@ int pfe_bates22(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* st
  * NULL/0); out = n x 3 fp64 [RMS of sub-band peak positions, mean pairwise correlation,
  * sum of profile correlations > 0.0055]; status bits PFE_ST_SUBBAND_FAIL where the
  * reference raises (boxcar width <= 0 or > nBins, every pair NaN, lp != lsb).
- * Any nsub in [2, 256] and lsb in [1, 1024] with nsub * (lsb + 1) <= 32768. */
+ * Any nsub in [1, 65536] and lsb in [1, 16384] (lp up to 16384 here): nsub 2-256 with
+ * nsub * (lsb + 1) <= 32768 on chip, every other shape through global scratch of the handle. */
 int pfe_subband3(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
                  uint32_t flags);
+
+/* One score group of the chain alone: the batched form of one method of the reference's
+ * second plug-in class, ProfileOperationsInterface (ProfileOperationsInterface.py:69-130),
+ * as PHCXOperations implements it.  `in` as for pfe_bates22, but only the arrays a group
+ * reads are used (the others may be NULL / 0); the same kernels, so every value is the bits
+ * the group's columns of pfe_bates22 hold; status carries that group's failure bit only.
+ *   pfe_sinusoid4 <- getSinusoidFittings(profile)        ProfileOperations.py:190-376
+ *                    reads prof; out n x 4 = s1-s4 (pfe_bates22 columns 0-3)
+ *   pfe_gauss7    <- getGaussianFittings(profile)        ProfileOperations.py:595-770
+ *                    reads prof; out n x 7 = s5-s11 (columns 4-10)
+ *   pfe_params4   <- getCandidateParameters(data, sec)   PHCXOperations.py:81-112
+ *                    reads scal; out n x 4 = [period_ms, snr, dm, width] as the method
+ *                    returns them (PHCXFile applies filterScore(13/14) for s13/s14)
+ *   pfe_dmfit4    <- getDMFittings(data, sec)            PHCXOperations.py:121-233
+ *                    reads dmcurve, scal; out n x 4 = [peak, |1 - Prop|, Shift, chi_theo]:
+ *                    the method's signed Shift (s18 = filterScore(18, Shift) = |Shift|) */
+int pfe_sinusoid4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                  uint32_t flags);
+int pfe_gauss7(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+               uint32_t flags);
+int pfe_params4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                uint32_t flags);
+int pfe_dmfit4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+               uint32_t flags);
 
 /* ---- PFD (PRESTO fold) files: preprocessing + Lyon features -------------------------
  * pfe_pfd_dmprof <- what a freshly loaded PFDFile computes for the dmprof path

@@ -405,8 +405,9 @@ DF = 400
 F = 1374
 
 
-def dm_scores(curve, scal):
-    """[s16..s19]  (PHCXOperations.py:150-233; filterScore(18) = abs)."""
+def dm_scores(curve, scal, signed_shift=False):
+    """[s16..s19]  (PHCXOperations.py:150-233; filterScore(18) = abs).  signed_shift: the
+    third value as getDMFittings returns it (plsq[0][2], :232), before PHCXFile's filter."""
     period, snr, dm, width = float(scal[0]), float(scal[1]), float(scal[2]), float(scal[3])
     dm_start, dm_end, length_all = float(scal[4]), float(scal[5]), int(scal[6])
     y = np.asarray(curve)
@@ -435,7 +436,8 @@ def dm_scores(curve, scal):
         if fit[i] >= 1.:
             chi += (y[i] - theo[i]) ** 2
     chi = chi / n
-    return [float(peak), float(abs(1 - p[1])), float(abs(float(p[2]))), float(chi)]
+    shift = float(p[2]) if signed_shift else float(abs(float(p[2])))
+    return [float(peak), float(abs(1 - p[1])), shift, float(chi)]
 
 
 # ---------------------------------------------------------------------------------------

@@ -43,6 +43,10 @@ EXPORTED_SYMBOLS = (
     "pfe_lyon8_f64",
     "pfe_bates22",
     "pfe_subband3",
+    "pfe_sinusoid4",
+    "pfe_gauss7",
+    "pfe_params4",
+    "pfe_dmfit4",
     "pfe_pfd_dmprof",
     "pfe_pfd_bates22",
 )
@@ -204,6 +208,9 @@ def load_library(path: str | None = None) -> C.CDLL:
         lib.pfe_bates22.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
         lib.pfe_subband3.restype = C.c_int
         lib.pfe_subband3.argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
+        for g in ("pfe_sinusoid4", "pfe_gauss7", "pfe_params4", "pfe_dmfit4"):
+            getattr(lib, g).restype = C.c_int
+            getattr(lib, g).argtypes = [vp, C.POINTER(BatesIn), vp, vp, u32]
         lib.pfe_pfd_dmprof.restype = C.c_int
         lib.pfe_pfd_dmprof.argtypes = [vp, C.POINTER(PfdIn), vp, vp, vp, vp, u32]
         lib.pfe_pfd_bates22.restype = C.c_int
@@ -527,6 +534,55 @@ class Engine:
         self._check(self.lib.pfe_subband3(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
         del keep
         return out, status
+
+    # ---- one score group (ProfileOperationsInterface.py:69-130; pfe.h per-group block) ----
+    def _group(self, fn, k, prof, dmcurve, scal, out, status):
+        n = scal.shape[0]
+        dev = _is_device(scal)
+        if dev:
+            import torch
+
+            for a, nm in ((prof, "prof"), (dmcurve, "dmcurve")):
+                if a is not None:
+                    self._dev(a, nm, (torch.uint8,) if nm == "prof" else (torch.float64,))
+            self._dev(scal, "scal", (torch.float64,))
+            self._follow_torch()
+            if out is None:
+                out = torch.empty((n, k), dtype=torch.float64, device=scal.device)
+            self._dev(out, "out", (torch.float64,), (n, k))
+            status = self._status_dev(status, n)
+            flags = PFE_FLAG_DEVICE_PTRS
+        else:
+            prof = None if prof is None else np.ascontiguousarray(prof, dtype=np.uint8)
+            dmcurve = None if dmcurve is None else np.ascontiguousarray(dmcurve, dtype=np.float64)
+            scal = np.ascontiguousarray(scal, dtype=np.float64)
+            out = self._out_host(out, n, k)
+            status = self._status_host(status, n)
+            flags = 0
+        for a in (prof, dmcurve):
+            if a is not None and a.shape[0] != n:
+                raise ValueError("inputs must have the same number of rows")
+        bi = BatesIn(_ptr(prof) if prof is not None else None, prof.shape[1] if prof is not None else 0,
+                     None, 0, 0, _ptr(dmcurve) if dmcurve is not None else None,
+                     dmcurve.shape[1] if dmcurve is not None else 0, _ptr(scal), n)
+        self._check(getattr(self.lib, fn)(self._h, C.byref(bi), _ptr(out), _ptr(status), flags))
+        return out, status
+
+    def sinusoid4(self, prof, scal, out=None, status=None):
+        """getSinusoidFittings (pfe_sinusoid4): s1-s4 -> ((n, 4), (n,) status)."""
+        return self._group("pfe_sinusoid4", 4, prof, None, scal, out, status)
+
+    def gauss7(self, prof, scal, out=None, status=None):
+        """getGaussianFittings (pfe_gauss7): s5-s11 -> ((n, 7), (n,) status)."""
+        return self._group("pfe_gauss7", 7, prof, None, scal, out, status)
+
+    def params4(self, scal, out=None, status=None):
+        """getCandidateParameters (pfe_params4): [period_ms, snr, dm, width], unfiltered."""
+        return self._group("pfe_params4", 4, None, None, scal, out, status)
+
+    def dmfit4(self, dmcurve, scal, out=None, status=None):
+        """getDMFittings (pfe_dmfit4): [peak, |1 - Prop|, Shift (signed), chi_theo]."""
+        return self._group("pfe_dmfit4", 4, None, dmcurve, scal, out, status)
 
     def features30(self, prof, lyon_dm, sub, dmcurve, scal, out=None):
         """Config 5's feature matrix: the 8 Lyon features (profile + Lyon DM rows) then the

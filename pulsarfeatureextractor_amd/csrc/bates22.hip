@@ -14,6 +14,7 @@ hipError_t launch_sine(const BatesArgs& a, hipStream_t st);
 hipError_t launch_gauss(const BatesArgs& a, hipStream_t st);
 hipError_t launch_dmfit(const BatesArgs& a, hipStream_t st);
 hipError_t launch_subband(const BatesArgs& a, hipStream_t st);
+size_t subband_work_bytes(int64_t n, int nsub, int lsb);
 
 static int device_cus() {
   int dev = 0, cus = 256;
@@ -76,14 +77,19 @@ static int wide_waves(int64_t n) {
 }
 
 // workspace layout: [GaussWS x n][counters][hand-over regions][wide queue][wide slabs]
-// [per-wave scratch]
-size_t bates22_workspace_bytes(const pfe_bates_in* in) {
+// [per-wave scratch] (bates_setup) then, for sub-band shapes the LDS kernels do not hold,
+// the any-shape sub-band kernel's slabs
+static size_t bates22_core_bytes(const pfe_bates_in* in) {
   size_t hb = 0;
   for (int r = 0; r < 3; ++r) hb += align256(hand_bytes(in->n, r, in->lp));
   return 256 + align256((size_t)in->n * sizeof(GaussWS)) +
          align256(BATES_NCOUNTERS * sizeof(unsigned)) + hb +
          align256((size_t)in->n * sizeof(int)) + (size_t)wide_waves(in->n) * WIDE_SLAB_BYTES +
          (size_t)persistent_waves(in->n) * gdg_wave_scratch_doubles(in->lp) * sizeof(double);
+}
+size_t bates22_workspace_bytes(const pfe_bates_in* in) {
+  const size_t sw = subband_work_bytes(in->n, in->nsub, in->lsb);
+  return bates22_core_bytes(in) + (sw ? 256 + align256(sw) : 0);
 }
 
 __global__ void k_clear_internal(uint32_t* status, int64_t n) {
@@ -114,6 +120,8 @@ void bates_setup(BatesArgs& a, int64_t n, int lp, void* work, const Options& o) 
   a.wide_scr = (double*)wb;
   a.wide_waves = wide_waves(n);
   wb += (size_t)a.wide_waves * WIDE_SLAB_BYTES;
+  a.sub_work = nullptr;  // set by the 22-score launcher, which knows the sub-band shape
+  a.raw_dm = 0;
   a.wscr = (double*)wb;
   a.pwaves = persistent_waves(n);
   a.fpw = blm_fits_per_wave(n, device_cus());
@@ -143,11 +151,18 @@ hipError_t fork_end(const Fork* fk, hipStream_t st) {
   return hipStreamWaitEvent(st, fk->ev[2], 0);
 }
 
-hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
-                          size_t work_bytes, hipStream_t st, const Fork* fk, const Options& o) {
+// The score groups `groups` (BG_*) of the chain, each into its own columns of out (n x 22);
+// status gets the failure bits of those groups only.  raw_dm: getDMFittings' signed shift in
+// column 17 (the per-group entry point pfe_dmfit4) instead of the 22-score vector's |shift|.
+hipError_t launch_bates_groups(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                               size_t work_bytes, hipStream_t st, const Fork* fk,
+                               const Options& o, unsigned groups, bool raw_dm) {
   if (work_bytes < bates22_workspace_bytes(in)) return hipErrorInvalidValue;
   BatesArgs a;
   bates_setup(a, in->n, in->lp, work, o);
+  a.raw_dm = raw_dm ? 1 : 0;
+  if (subband_work_bytes(in->n, in->nsub, in->lsb))
+    a.sub_work = (void*)(((uintptr_t)work + bates22_core_bytes(in) + 255) & ~(uintptr_t)255);
   a.prof = in->prof;
   a.fprof = nullptr;
   a.lp = in->lp;
@@ -166,20 +181,25 @@ hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status,
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.counters, 0, BATES_NCOUNTERS * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
-  if (fork_begin(fk, st)) {
+  if (groups == BG_ALL && fork_begin(fk, st)) {
     if ((e = launch_gauss(a, fk->side[0])) != hipSuccess) return e;
     if ((e = launch_dmfit(a, fk->side[1])) != hipSuccess) return e;
     if ((e = launch_subband(a, fk->side[1])) != hipSuccess) return e;
     if ((e = launch_sine(a, st)) != hipSuccess) return e;
     if ((e = fork_end(fk, st)) != hipSuccess) return e;
   } else {
-    if ((e = launch_sine(a, st)) != hipSuccess) return e;
-    if ((e = launch_gauss(a, st)) != hipSuccess) return e;
-    if ((e = launch_dmfit(a, st)) != hipSuccess) return e;
-    if ((e = launch_subband(a, st)) != hipSuccess) return e;
+    if ((groups & BG_SINE) && (e = launch_sine(a, st)) != hipSuccess) return e;
+    if ((groups & BG_GAUSS) && (e = launch_gauss(a, st)) != hipSuccess) return e;
+    if ((groups & BG_DM) && (e = launch_dmfit(a, st)) != hipSuccess) return e;
+    if ((groups & BG_SUB) && (e = launch_subband(a, st)) != hipSuccess) return e;
   }
   launch_clear_internal(status, in->n, st);
   return hipGetLastError();
+}
+
+hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                          size_t work_bytes, hipStream_t st, const Fork* fk, const Options& o) {
+  return launch_bates_groups(in, out, status, work, work_bytes, st, fk, o, BG_ALL, false);
 }
 
 }  // namespace pfe

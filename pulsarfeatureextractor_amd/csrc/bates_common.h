@@ -70,7 +70,12 @@ struct BatesArgs {
   int* wide_list;      // candidates queued for k_ghist_wide (n entries)
   double* wide_scr;    // per-wave row scratch of k_ghist_wide (wide_waves slabs)
   int wide_waves;
+  void* sub_work;       // scratch of the any-shape sub-band kernel (subband_work_bytes), or null
+  int raw_dm;           // 1: column 17 holds getDMFittings' signed shift, not filterScore(18, .)
 };
+
+// score groups of the chain (launch_bates_groups): the ProfileOperationsInterface methods
+enum : unsigned { BG_SINE = 1u, BG_GAUSS = 2u, BG_DM = 4u, BG_SUB = 8u, BG_ALL = 15u };
 
 constexpr int BATES_NCOUNTERS = 16;
 // Hand-over scratch (lm_group.h HandOver): one region per concurrently running chain, sized

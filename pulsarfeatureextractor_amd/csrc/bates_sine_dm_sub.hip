@@ -549,7 +549,8 @@ __device__ __forceinline__ void dm_finish(const BatesArgs& a, int64_t c, const D
     o[14] = width;                                                   // s15
     o[15] = snr / sqrt((period - sqrt(wint)) / sqrt(wint));          // s16 (:191)
     o[16] = fabs(1.0 - p[1]);                                        // s17
-    o[17] = fabs(p[2]);                                              // s18 (filterScore 18)
+    // s18 = filterScore(18, shift) = |shift|; getDMFittings itself returns the signed shift
+    o[17] = a.raw_dm ? p[2] : fabs(p[2]);
     o[18] = chi;                                                     // s19
   }
 }

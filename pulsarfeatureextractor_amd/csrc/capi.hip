@@ -29,8 +29,13 @@ hipError_t launch_lyon8_f64(const double* prof, int64_t ps, int lp, const double
 hipError_t launch_bates22(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
                           size_t work_bytes, hipStream_t st, const Fork* fk, const Options& o);
 size_t bates22_workspace_bytes(const pfe_bates_in* in);
-hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, hipStream_t st);
+hipError_t launch_bates_groups(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                               size_t work_bytes, hipStream_t st, const Fork* fk,
+                               const Options& o, unsigned groups, bool raw_dm);
+hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                           hipStream_t st);
 const char* subband_shape_error(int nsub, int lsb);
+size_t subband_work_bytes(int64_t n, int nsub, int lsb);
 }  // namespace pfe
 
 // chunked host path: device/staging slots in flight (H2D of k+1 | kernel k | D2H of k-1)
@@ -492,8 +497,11 @@ int pfe_lyon8_f64(pfe_handle* h, const double* prof, int64_t ps, int32_t lp, con
 static int check_bates_in(pfe_handle* h, const pfe_bates_in* in, const char* fn, bool need_dm) {
   if (!in->prof || !in->sub || !in->scal || (need_dm && !in->dmcurve))
     return set_err(h, PFE_EINVAL, "%s: null input array", fn);
-  if (in->lp < 8 || in->lp > 1024)
-    return set_err(h, PFE_EINVAL, "%s: lp=%d outside [8,1024]", fn, in->lp);
+  // the 22-score chain's profile kernels take 8-1024 bins; the sub-band scores alone only
+  // compare the profile with the sub-bands (any nBins the any-shape kernel holds)
+  if (need_dm ? (in->lp < 8 || in->lp > 1024) : (in->lp < 1 || in->lp > 16384))
+    return set_err(h, PFE_EINVAL, "%s: lp=%d outside [%d,%d]", fn, in->lp, need_dm ? 8 : 1,
+                   need_dm ? 1024 : 16384);
   // pfe_subband3 computes nothing else, so an unsupported sub-band shape fails the call; in
   // pfe_bates22 it only fails the rows' sub-band group (PFE_ST_UNSUPPORTED per row)
   if (!need_dm) {
@@ -600,17 +608,172 @@ int pfe_subband3(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* s
   double* dout = out;
   uint32_t* dstat = status;
   size_t off = 0;
+  const size_t work = pfe::subband_work_bytes(n, in->nsub, in->lsb);
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
-    rc = stage_bates(h, in, din, 3, false, 0, dout, dstat, off);
-    if (rc) return rc;
+    rc = stage_bates(h, in, din, 3, false, work ? work + 256 : 0, dout, dstat, off);
+  } else if (work) {
+    rc = ensure_scratch(h, work + 256);
   }
-  hipError_t e = pfe::launch_subband3(&din, dout, dstat, st);
+  if (rc) return rc;
+  void* wp = work ? (void*)(((uintptr_t)h->scratch + off + 255) & ~(uintptr_t)255) : nullptr;
+  hipError_t e = pfe::launch_subband3(&din, dout, dstat, wp, st);
   if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "subband3 launch: %s", hipGetErrorString(e));
   if (!(flags & PFE_FLAG_DEVICE_PTRS)) {
     PFE_HIP(h, hipMemcpyAsync(out, dout, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipMemcpyAsync(status, dstat, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PFE_HIP(h, hipStreamSynchronize(st));
   }
+  return call_end(h);
+}
+
+}  // extern "C"
+
+// ---- one score group of the chain (ProfileOperationsInterface.py:69-130) ----------------
+// columns [c0, c0 + k) of the 22-score vector -> dst (n x k)
+__global__ void k_take_cols(const double* src, int c0, int k, int64_t n, double* dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * k) dst[i] = src[(i / k) * 22 + c0 + i % k];
+}
+
+// getCandidateParameters: (period, snr, dm, width) of each candidate, unfiltered
+__global__ void k_params4(const double* scal, int64_t n, double* out, uint32_t* status) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* sc = scal + i * PFE_NSCAL;
+  out[i * 4 + 0] = sc[PFE_SCAL_PERIOD_MS];
+  out[i * 4 + 1] = sc[PFE_SCAL_SNR];
+  out[i * 4 + 2] = sc[PFE_SCAL_DM];
+  out[i * 4 + 3] = sc[PFE_SCAL_WIDTH];
+  status[i] = 0;
+}
+
+// groups: pfe::BG_SINE (cols 0-3) / BG_GAUSS (4-10) / BG_DM (15-18, raw shift)
+static int bates_group_call(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                            uint32_t flags, const char* fn, unsigned groups, int c0, int k) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  if (!in || !out || !status) return set_err(h, PFE_EINVAL, "%s: null argument", fn);
+  const int64_t n = in->n;
+  if (n < 0) return set_err(h, PFE_EINVAL, "%s: n < 0", fn);
+  if (n == 0) return PFE_OK;
+  const bool dm = groups == pfe::BG_DM;
+  if (!in->scal || (dm ? !in->dmcurve : !in->prof))
+    return set_err(h, PFE_EINVAL, "%s: null input array", fn);
+  if (!dm && (in->lp < 8 || in->lp > 1024))
+    return set_err(h, PFE_EINVAL, "%s: lp=%d outside [8,1024]", fn, in->lp);
+  if (dm && (in->ndm < 3 || in->ndm > 1024))
+    return set_err(h, PFE_EINVAL, "%s: ndm=%d outside [3,1024]", fn, in->ndm);
+  int rc = call_begin(h);
+  if (rc) return rc;
+  hipStream_t st = h->stream;
+  // only the arrays the group reads; no sub-band work
+  pfe_bates_in g = *in;
+  g.sub = nullptr;
+  g.nsub = g.lsb = 0;
+  if (dm) {
+    g.prof = nullptr;
+    g.lp = 0;
+  } else {
+    g.dmcurve = nullptr;
+    g.ndm = 0;
+  }
+  const bool host = !(flags & PFE_FLAG_DEVICE_PTRS);
+  const size_t work = pfe::bates22_workspace_bytes(&g);
+  const size_t pb = host && !dm ? align256((size_t)n * g.lp) : 0;
+  const size_t db = host && dm ? align256((size_t)n * g.ndm * sizeof(double)) : 0;
+  const size_t cb = host ? align256((size_t)n * PFE_NSCAL * sizeof(double)) : 0;
+  const size_t ob = align256((size_t)n * 22 * sizeof(double));
+  const size_t kb = host ? align256((size_t)n * k * sizeof(double)) : 0;
+  const size_t tb = host ? align256((size_t)n * sizeof(uint32_t)) : 0;
+  rc = ensure_scratch(h, pb + db + cb + ob + kb + tb + work + 256);
+  if (rc) return rc;
+  char* base = (char*)(((uintptr_t)h->scratch + 255) & ~(uintptr_t)255);
+  pfe_bates_in din = g;
+  size_t off = 0;
+  if (host) {
+    if (dm) {
+      PFE_HIP(h, hipMemcpyAsync(base, in->dmcurve, (size_t)n * g.ndm * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+      din.dmcurve = (const double*)base;
+    } else {
+      PFE_HIP(h, hipMemcpyAsync(base, in->prof, (size_t)n * g.lp, hipMemcpyHostToDevice, st));
+      din.prof = (const uint8_t*)base;
+    }
+    off = pb + db;
+    PFE_HIP(h, hipMemcpyAsync(base + off, in->scal, (size_t)n * PFE_NSCAL * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    din.scal = (const double*)(base + off);
+    off += cb;
+  }
+  double* d22 = (double*)(base + off);
+  off += ob;
+  double* dk = host ? (double*)(base + off) : out;
+  off += kb;
+  uint32_t* dst = host ? (uint32_t*)(base + off) : status;
+  off += tb;
+  hipError_t e = pfe::launch_bates_groups(&din, d22, dst, base + off, work, st, &h->fork, h->opt,
+                                          groups, dm);
+  if (e != hipSuccess) return set_err(h, PFE_EDEVICE, "%s launch: %s", fn, hipGetErrorString(e));
+  hipLaunchKernelGGL(k_take_cols, dim3((unsigned)((n * k + 255) / 256)), dim3(256), 0, st, d22,
+                     c0, k, n, dk);
+  PFE_HIP(h, hipGetLastError());
+  if (host) {
+    PFE_HIP(h, hipMemcpyAsync(out, dk, (size_t)n * k * sizeof(double), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipMemcpyAsync(status, dst, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PFE_HIP(h, hipStreamSynchronize(st));
+  }
+  return call_end(h);
+}
+
+extern "C" {
+
+int pfe_sinusoid4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                  uint32_t flags) {
+  return bates_group_call(h, in, out, status, flags, "sinusoid4", pfe::BG_SINE, 0, 4);
+}
+
+int pfe_gauss7(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+               uint32_t flags) {
+  return bates_group_call(h, in, out, status, flags, "gauss7", pfe::BG_GAUSS, 4, 7);
+}
+
+int pfe_dmfit4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+               uint32_t flags) {
+  return bates_group_call(h, in, out, status, flags, "dmfit4", pfe::BG_DM, 15, 4);
+}
+
+int pfe_params4(pfe_handle* h, const pfe_bates_in* in, double* out, uint32_t* status,
+                uint32_t flags) {
+  if (!h) return PFE_EINVAL;
+  h->err.clear();
+  if (!in || !out || !status || (in->n > 0 && !in->scal))
+    return set_err(h, PFE_EINVAL, "params4: null argument");
+  const int64_t n = in->n;
+  if (n < 0) return set_err(h, PFE_EINVAL, "params4: n < 0");
+  if (n == 0) return PFE_OK;
+  int rc = call_begin(h);
+  if (rc) return rc;
+  hipStream_t st = h->stream;
+  if (flags & PFE_FLAG_DEVICE_PTRS) {
+    hipLaunchKernelGGL(k_params4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in->scal,
+                       n, out, status);
+    PFE_HIP(h, hipGetLastError());
+    return call_end(h);
+  }
+  const size_t cb = align256((size_t)n * PFE_NSCAL * sizeof(double));
+  const size_t ob = align256((size_t)n * 4 * sizeof(double));
+  rc = ensure_scratch(h, cb + ob + (size_t)n * sizeof(uint32_t));
+  if (rc) return rc;
+  char* base = (char*)h->scratch;
+  PFE_HIP(h, hipMemcpyAsync(base, in->scal, (size_t)n * PFE_NSCAL * sizeof(double),
+                            hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_params4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (const double*)base, n, (double*)(base + cb), (uint32_t*)(base + cb + ob));
+  PFE_HIP(h, hipGetLastError());
+  PFE_HIP(h, hipMemcpyAsync(out, base + cb, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+  PFE_HIP(h, hipMemcpyAsync(status, base + cb + ob, (size_t)n * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, st));
+  PFE_HIP(h, hipStreamSynchronize(st));
   return call_end(h);
 }
 

@@ -9,7 +9,8 @@
 //        skipped, ZeroDivisionError when none is left            (:1663-1675)
 //   s22  sum of |corrcoef(sub-band j, profile)| over the values > 0.0055 (:403-415, :345-347)
 //
-// Design (one wave per candidate, any nsub, nBins up to 1024):
+// Design (one wave per candidate; nsub 2-256, nBins up to 1024 on chip, any other shape up
+// to 65536 x 16384 through k_subband_g and global scratch):
 //   * The candidate's nsub x lsb sub-band bytes are read once (16 B per lane, coalesced) and
 //     turned into per-band exclusive prefix sums E[i][t] = sum_{u<t} x[i][u] in LDS (u16 up
 //     to 256 bins, else u32): a 16-byte piece is prefixed in the lane with v_dot4, the
@@ -662,13 +663,158 @@ void k_subband_fast(SubArgs a) {
   }
 }
 
+// ---- any shape: prefix rows in global scratch -------------------------------------------
+// The LDS-resident kernels above hold a candidate's nsub x (lsb + 1) prefix sums on chip
+// (nsub 2-256, nBins 1-1024, nsub (nBins + 1) <= 32768).  Every other shape the reference
+// scores (getSubband_scores takes any nsub x nBins) goes here: persistent waves, each with a
+// slab of global scratch holding ONE band's prefix row at a time (E, lsb + 1 u32), the s21
+// window sums Z (nw doubles, lane-owned) and the boxcar-maximum positions (nsub ints).  The
+// arithmetic is k_subband2's, band by band: integer boxcar sums and keys (64-bit here, any
+// window index), exact S / nw sum b^2 - S^2 (128-bit), the same z-score identity for s21, and
+// s22's centred fp64 sums in the same per-lane slot order and butterfly.
+constexpr int SBG_MAX_NSUB = 65536, SBG_MAX_LSB = 16384;
+
+__host__ __device__ inline size_t sbg_slab_bytes(int nsub, int lsb) {
+  return ((size_t)(lsb + 1) * 4 + 15) / 16 * 16 + (size_t)lsb * 8 + ((size_t)nsub * 4 + 15) / 16 * 16;
+}
+static int64_t sbg_waves(int64_t n) { return n < 1024 ? (n > 0 ? n : 1) : 1024; }
+
+__device__ __forceinline__ unsigned long long wmax_u64(unsigned long long v) {
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const unsigned long long o = (unsigned long long)__shfl_xor((long long)v, s);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void sbg_sync() {  // the wave's global-scratch stores -> its loads
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64) void k_subband_g(SubArgs a, unsigned char* work) {
+  const int lane = lane_id();
+  const int nsub = a.nsub, lsb = a.lsb;
+  unsigned char* slab = work + (size_t)blockIdx.x * sbg_slab_bytes(nsub, lsb);
+  uint32_t* E = reinterpret_cast<uint32_t*>(slab);
+  double* Zg = reinterpret_cast<double*>(slab + ((size_t)(lsb + 1) * 4 + 15) / 16 * 16);
+  int* maxbin = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(Zg) + (size_t)lsb * 8);
+  for (int64_t c = blockIdx.x; c < a.n; c += gridDim.x) {
+    sbg_sync();  // the previous candidate's reads of Zg / maxbin precede this one's stores
+    const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
+    const double wbd = ceil(width * (double)lsb);                    // :1603
+    if (!(wbd >= 1.0) || wbd > (double)lsb || a.lp != lsb) {
+      if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+      continue;
+    }
+    const int wb = (int)wbd;
+    const int nw = lsb - wb + 1;
+    const uint8_t* sb = a.sub + c * (int64_t)nsub * lsb;
+    const uint8_t* pr = a.prof + c * a.lp;
+    // the profile, centred as numpy.corrcoef centres it (s22): slots j = lane + 64 k in order
+    double pm = 0.0;
+    for (int j = lane; j < lsb; j += 64) pm += (double)pr[j];
+    pm = wsum(pm) / (double)lsb;
+    double pvar = 0.0;
+    for (int j = lane; j < lsb; j += 64) {
+      const double v = (double)pr[j] - pm;
+      pvar += v * v;
+    }
+    pvar = wsum(pvar);
+    const double inv2 = 1.0 / (double)(lsb - 1);
+    for (int j = lane; j < nw; j += 64) Zg[j] = 0.0;
+    const double dnw = (double)nw;
+    double zz = 0.0, integ = 0.0;
+    int valid = 0;
+    for (int i = 0; i < nsub; ++i) {
+      const uint8_t* row = sb + (size_t)i * lsb;
+      sbg_sync();  // every lane is done with the previous band's E
+      uint32_t carry = 0;
+      for (int base = 0; base < lsb; base += 64) {
+        const int t = base + lane;
+        const int x = t < lsb ? (int)row[t] : 0;
+        const int ex = wscan_excl(x);
+        if (t < lsb) E[t] = carry + (uint32_t)ex;
+        carry += (uint32_t)__shfl(ex + x, 63);
+      }
+      if (lane == 0) E[lsb] = carry;
+      sbg_sync();
+      // boxcar statistics: S, sum b^2, first strict maximum
+      long long S = 0, Q = 0;
+      unsigned long long key = 0;
+      for (int j = lane; j < nw; j += 64) {
+        const long long b = (long long)E[j + wb] - (long long)E[j];
+        S += b;
+        Q += b * b;
+        const unsigned long long kk = ((unsigned long long)b << 32) | (0xFFFFFFFFull - (unsigned)j);
+        key = kk > key ? kk : key;
+      }
+      S = wsum_ll(S);
+      Q = wsum_ll(Q);
+      key = wmax_u64(key);
+      const __int128 N = (__int128)nw * Q - (__int128)S * S;          // exact: nw^2 var(b)
+      const double r = N > 0 ? 1.0 / sqrt(dnw * (double)N) : 0.0;
+      valid += N > 0 ? 1 : 0;
+      if (lane == 0) maxbin[i] = (int)(0xFFFFFFFFull - (key & 0xFFFFFFFFull)) + wb / 2;  // :1628
+      if (r != 0.0) {
+        for (int j = lane; j < nw; j += 64) {
+          const long long b = (long long)E[j + wb] - (long long)E[j];
+          const double z = (double)((long long)nw * b - S) * r;
+          Zg[j] += z;
+          zz += z * z;
+        }
+      }
+      const double mu = (double)E[lsb] / (double)lsb;
+      double dd = 0.0, q = 0.0;
+      for (int j = lane; j < lsb; j += 64) {
+        const double t = (double)((int)E[j + 1] - (int)E[j]) - mu;
+        dd += t * ((double)pr[j] - pm);
+        q += t * t;
+      }
+      dd = wsum(dd);
+      q = wsum(q);
+      const double cc = fabs(sb_corr(dd * inv2, q * inv2, pvar * inv2));
+      if (cc > 0.0055) integ += cc;                                   // in band order
+    }
+    double zs = 0.0;
+    for (int j = lane; j < nw; j += 64) zs += Zg[j] * Zg[j];
+    zs = wsum(zs);
+    zz = wsum(zz);
+    const long long m = (long long)valid * (valid - 1) / 2;
+    if (m == 0) {  // ZeroDivisionError (:1681)
+      if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
+      continue;
+    }
+    const double mean_corr = (0.5 * (zs - zz)) / (double)m;
+    sbg_sync();
+    const double rms = rms_of_maxbins(maxbin, nsub, wb);
+    if (lane == 0) {
+      double* o = a.out + c * a.ldo;
+      o[0] = rms;
+      o[1] = mean_corr;
+      o[2] = integ;
+    }
+  }
+}
+
 // ---- launchers -------------------------------------------------------------------------
+// the LDS-resident kernels' shapes
+static bool subband_lds_shape(int nsub, int lsb) {
+  return nsub >= 2 && nsub <= 256 && lsb >= 1 && lsb <= 1024 && (int64_t)nsub * (lsb + 1) <= 32768;
+}
+
 // nullptr when the shape is scored, else why not (checked by the C-ABI before any launch)
 const char* subband_shape_error(int nsub, int lsb) {
-  if (nsub < 2 || nsub > 256) return "nsub outside [2, 256]";
-  if (lsb < 1 || lsb > 1024) return "lsb outside [1, 1024]";
-  if ((int64_t)nsub * (lsb + 1) > 32768) return "nsub * (lsb + 1) exceeds 32768 (LDS-resident limit)";
+  if (nsub < 1 || nsub > SBG_MAX_NSUB) return "nsub outside [1, 65536]";
+  if (lsb < 1 || lsb > SBG_MAX_LSB) return "lsb outside [1, 16384]";
   return nullptr;
+}
+
+// global scratch of the any-shape kernel for n candidates (0: the LDS kernels take the shape)
+size_t subband_work_bytes(int64_t n, int nsub, int lsb) {
+  if (subband_lds_shape(nsub, lsb) || subband_shape_error(nsub, lsb)) return 0;
+  return (size_t)sbg_waves(n) * sbg_slab_bytes(nsub, lsb);
 }
 
 template <int SL, typename PT>
@@ -699,9 +845,15 @@ static hipError_t launch_fast(const SubArgs& s, hipStream_t st) {
   return hipGetLastError();
 }
 
-static hipError_t launch_sub(const SubArgs& s, hipStream_t st) {
+static hipError_t launch_sub(const SubArgs& s, void* work, hipStream_t st) {
   if (s.n <= 0) return hipSuccess;
   if (subband_shape_error(s.nsub, s.lsb)) return hipErrorInvalidValue;
+  if (!subband_lds_shape(s.nsub, s.lsb)) {
+    if (!work) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_subband_g, dim3((unsigned)sbg_waves(s.n)), dim3(64), 0, st, s,
+                       (unsigned char*)work);
+    return hipGetLastError();
+  }
   const int L = s.lsb;
   const bool aligned = (((uintptr_t)s.sub | (uintptr_t)s.prof) & 15) == 0;
   if (aligned && s.lp == L) {
@@ -727,8 +879,9 @@ __global__ void k_mark_unsupported(uint32_t* status, int64_t n) {
 }
 
 // the 22-score chain: scores 20-22 into columns 19-21 of out (n x 22).  A sub-band shape
-// the kernels do not hold (subband_shape_error) fails its rows, not the call: the other
-// groups' scores are still computed and every row gets PFE_ST_UNSUPPORTED.
+// beyond every kernel (subband_shape_error: nsub > 65536 or nBins > 16384) fails its rows,
+// not the call: the other groups' scores are still computed and every row gets
+// PFE_ST_UNSUPPORTED.  a.sub_work: the any-shape kernel's scratch (subband_work_bytes)
 hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   if (subband_shape_error(a.nsub, a.lsb)) {
@@ -737,17 +890,18 @@ hipError_t launch_subband(const BatesArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   SubArgs s{a.prof, a.lp, a.sub, a.nsub, a.lsb, a.scal, a.n, a.out + 19, 22, a.status};
-  return launch_sub(s, st);
+  return launch_sub(s, a.sub_work, st);
 }
 
-// pfe_subband3: out n x 3; status zeroed here
-hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, hipStream_t st) {
+// pfe_subband3: out n x 3; status zeroed here; work: subband_work_bytes(n, nsub, lsb) bytes
+hipError_t launch_subband3(const pfe_bates_in* in, double* out, uint32_t* status, void* work,
+                           hipStream_t st) {
   hipError_t e = hipMemsetAsync(status, 0, (size_t)in->n * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(out, 0, (size_t)in->n * 3 * sizeof(double), st);
   if (e != hipSuccess) return e;
   SubArgs s{in->prof, in->lp, in->sub, in->nsub, in->lsb, in->scal, in->n, out, 3, status};
-  return launch_sub(s, st);
+  return launch_sub(s, work, st);
 }
 
 }  // namespace pfe

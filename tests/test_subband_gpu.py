@@ -171,27 +171,46 @@ def test_nsub32_vs_reference_golden(engine):
     assert np.array_equal((st & 0xFF) == 0, ok)
 
 
-@pytest.mark.parametrize("nsub,lsb", [(32, 1024), (64, 512), (300, 8)])
-def test_unsupported_subband_shape_fails_rows_not_call(engine, nsub, lsb):
-    """A sub-band shape the kernels do not hold (nsub*(lsb+1) > 32768 or nsub > 256) no
-    longer fails the whole pfe_bates22 call: every row gets PFE_ST_UNSUPPORTED and the other
-    score groups are computed exactly as for the same candidates with a supported shape.
-    pfe_subband3 (nothing else to compute) still refuses the call."""
+@pytest.mark.parametrize("nsub,lsb,n", [(32, 1024, 10), (64, 512, 10), (300, 8, 10), (1, 64, 4),
+                                        (12, 1500, 4), (4, 3000, 3)])
+def test_any_shape_subband_vs_oracle(engine, nsub, lsb, n):
+    """Sub-band shapes the LDS-resident kernels do not hold (nsub > 256, nsub (nBins + 1) >
+    32768, nBins > 1024, nsub = 1) through the global-scratch kernel (k_subband_g): the
+    reference scores any shape, so these are parity tests against the oracle -- pfe_subband3
+    and columns 19-21 of pfe_bates22 (where lp = nBins fits the 22-score kernels), adversarial
+    rows included.  Windows of <= 10 % keep the oracle's pure-Python boxcar loop short."""
+    b = bates_batch(n, lp=min(lsb, 1024), nsub=16, lsb=min(lsb, 1024), seed=600 + nsub + lsb)
+    rng = np.random.default_rng(nsub * 7 + lsb)
+    sub = rng.integers(0, 256, (n, nsub, lsb), dtype=np.uint8)
+    sub[:, :, lsb // 3: lsb // 3 + max(1, lsb // 20)] += 40  # a common bright window
+    prof = rng.integers(0, 256, (n, lsb), dtype=np.uint8)
+    scal = b["scal"].copy()
+    scal[:, 3] = rng.uniform(0.5 / lsb, 0.1, size=n)
+    b2 = {"sub": sub, "scal": scal}
+    if n >= 9:
+        b2 = adversarial(b2)
+    out, st = engine.subband3(prof, b2["sub"], b2["scal"])
+    ref, ok = oracle_sub(prof, b2["sub"], b2["scal"])
+    check(out, st, ref, ok, f"{nsub}x{lsb}", lsb)
+    if lsb <= 1024 and lsb >= 8:
+        o22, s22 = engine.bates22(prof, b2["sub"], b["dmcurve"], b2["scal"])
+        assert not (s22 & 0x10).any()
+        assert np.array_equal((s22 & 0x08) == 0, ok)
+        assert np.array_equal(o22[ok][:, 19:22], out[ok])
+
+
+def test_subband_shape_beyond_every_kernel_fails_rows_not_call(engine):
+    """nsub > 65536: pfe_bates22 marks every row PFE_ST_UNSUPPORTED and still computes the
+    other score groups exactly as for the same candidates with an ordinary sub-band shape;
+    pfe_subband3 (nothing else to compute) refuses the call."""
     from pulsarfeatureextractor_amd._native import PfeError
 
-    b = bates_batch(64, lp=128, nsub=16, lsb=128, seed=77)
-    rng = np.random.default_rng(3)
-    big = rng.integers(0, 256, (64, nsub, lsb), dtype=np.uint8)
-    o, st = engine.bates22(b["prof"], big, b["dmcurve"], b["scal"])
+    b = bates_batch(8, lp=128, nsub=16, lsb=128, seed=77)
+    big = np.random.default_rng(3).integers(0, 256, (8, 65537, 2), dtype=np.uint8)
     ref, rst = engine.bates22(b["prof"], b["sub"], b["dmcurve"], b["scal"])
+    o, st = engine.bates22(b["prof"], big, b["dmcurve"], b["scal"])
     assert ((st & 0x10) != 0).all()
     assert np.array_equal(st & ~np.uint32(0x18), rst & ~np.uint32(0x18))
-    # with the score groups concurrent, a group may skip a row another group has already
-    # failed (its outputs are dropped anyway); in order (serial=1) every group runs fully,
-    # and the other groups' scores are the supported shape's, bit for bit
-    with engine.options(serial=1):
-        o, st = engine.bates22(b["prof"], big, b["dmcurve"], b["scal"])
-    assert ((st & 0x10) != 0).all()
     assert np.array_equal(o[:, :19], ref[:, :19], equal_nan=True)
     with pytest.raises(PfeError):
         engine.subband3(b["prof"], big, b["scal"])
