@@ -744,9 +744,28 @@ struct DmShape {
   int lp;          // profile length (64 / 128 / 256)
   int ld;          // DataBlock row length (multiple of 16)
   int len_last;    // bytes of the last chunk
-  int leaves_last; // leaves of the last chunk (power of two <= 64)
+  int leaves_last; // leaves of the last chunk (power of two <= 64; 48 in the tri form)
+  int tri;         // 1: the last chunk is 4224 bytes (nDM = 33 mod 64), numpy's one tree
+                   // with leaves at two depths: 16 blocks of 264 = 128 + (64 + 72)
   uint16_t start[DM_MAX_LEAVES + 1];  // leaf starts of the last chunk (+ its length)
 };
+
+// lane of leaf L of the last chunk: L itself, or in the tri form lane 4b + i for leaf i of
+// block b (lane 4b + 3 idle), so that a quad holds one 264-byte block
+__host__ __device__ inline int dm_leaf_lane(const DmShape& sh, int L) {
+  return sh.tri ? 4 * (L / 3) + L % 3 : L;
+}
+
+// numpy's sum of the last chunk's 48 leaves in the tri form: each quad's block as
+// L0 + (L64 + L72) (quad broadcasts, every lane of the quad gets the same bits), then the
+// 16 blocks pairwise as wave_sum_f64's upper levels
+__device__ __forceinline__ double wave_sum_tri_f64(double v) {
+  const double l0 = dpp_f64<0x00>(v), l1 = dpp_f64<0x55>(v), l2 = dpp_f64<0xAA>(v);
+  v = l0 + (l1 + l2);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f64<DPP_ROW_MIRROR>(v);
+  return row_total_f64(v);
+}
 
 constexpr int DM_S = 132;                     // LDS leaf stride
 constexpr int DM_IMG_BYTES = 64 * DM_S;       // one chunk image per wave (8448 B)
@@ -881,7 +900,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
     if (o < sh.len_last) {
       int L = 0;
       while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
-      a = (uint16_t)(L * DM_S + (o - sh.start[L]));
+      a = (uint16_t)(dm_leaf_lane(sh, L) * DM_S + (o - sh.start[L]));
     }
     stab[e] = a;
   }
@@ -896,7 +915,10 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
 #pragma unroll
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
-  const int nw_last = lane < sh.leaves_last ? (sh.start[lane + 1] - sh.start[lane]) >> 3 : 16;
+  // this lane's leaf of the last chunk (-1: none) and its 8-byte words
+  const int leaf_last = sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
+                               : (lane < sh.leaves_last ? lane : -1);
+  const int nw_last = leaf_last >= 0 ? (sh.start[leaf_last + 1] - sh.start[leaf_last]) >> 3 : 16;
   // dm_leaf's constants: eight zeros held in registers (the high halves of the byte pairs)
   // and 2^1023 in an SGPR pair (a VOP3 operand; as a literal it would cost a move per byte)
   uint32_t z[8];
@@ -968,14 +990,15 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         double l3, l4;
         double leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
-          const bool in = lane < sh.leaves_last;
+          const bool in = leaf_last >= 0;
           leaf = in ? leaf : 0.0;
           l3 = in ? l3 : 0.0;
           l4 = in ? l4 : 0.0;
         }
         a3 += l3;
         a4 += l4;
-        const double cs = wave_sum_f64(leaf);  // numpy's tree over the lane-ordered leaves
+        // numpy's tree over the lane-ordered leaves (the tri form: two depths)
+        const double cs = (ch == NCH - 1 && sh.tri) ? wave_sum_tri_f64(leaf) : wave_sum_f64(leaf);
         ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order (all scaled by 2^-102)
         wave_lds_sync();
       }
@@ -1154,19 +1177,34 @@ static void np_leaves(int off, int n, int depth, int* start, int* len, int* dep,
 
 // lyon8_u8_dm's layout of a DataBlock row of ld bytes: nch chunks of 8192 values, the last
 // one a perfect pairwise tree (all leaves at one depth) of <= 64 leaves of 64..128 values
+// (the one imperfect last chunk of a DataBlock, 4224 bytes at nDM = 33 mod 64, takes the
+// tri form: its 48 leaves are 16 blocks of 128 @ depth 5 + (64 + 72) @ depth 6)
 static bool dm_shape(int lp, int ld, DmShape& sh, int& nch) {
   if (ld <= 256 || ld > 4 * 8192 || ld % 16) return false;
   nch = (ld + 8191) / 8192;
   const int len = ld - 8192 * (nch - 1);
   int start[DM_MAX_LEAVES], lens[DM_MAX_LEAVES], dep[DM_MAX_LEAVES], cnt = 0;
   np_leaves(0, len, 0, start, lens, dep, cnt, DM_MAX_LEAVES);
-  if (cnt > DM_MAX_LEAVES || (cnt & (cnt - 1)) != 0) return false;
-  for (int i = 0; i < cnt; ++i)
-    if (dep[i] != dep[0] || lens[i] % 8 || lens[i] < 64 || lens[i] > 128) return false;
+  if (cnt > DM_MAX_LEAVES) return false;
+  bool tri = false;
+  if (cnt == 48) {  // the tri form, checked leaf by leaf
+    tri = true;
+    for (int i = 0; i < cnt; ++i) {
+      const int b = i / 3, k = i % 3;
+      tri = tri && start[i] == 264 * b + (k == 0 ? 0 : k == 1 ? 128 : 192) &&
+            lens[i] == (k == 0 ? 128 : k == 1 ? 64 : 72) && dep[i] == dep[0] + (k == 0 ? 0 : 1);
+    }
+    if (!tri) return false;
+  } else {
+    if ((cnt & (cnt - 1)) != 0) return false;
+    for (int i = 0; i < cnt; ++i)
+      if (dep[i] != dep[0] || lens[i] % 8 || lens[i] < 64 || lens[i] > 128) return false;
+  }
   sh.lp = lp;
   sh.ld = ld;
   sh.len_last = len;
   sh.leaves_last = cnt;
+  sh.tri = tri ? 1 : 0;
   for (int i = 0; i < cnt; ++i) sh.start[i] = (uint16_t)start[i];
   for (int i = cnt; i <= DM_MAX_LEAVES; ++i) sh.start[i] = (uint16_t)len;
   return true;

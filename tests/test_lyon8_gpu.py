@@ -197,14 +197,16 @@ def test_long_dm_rows_other_lengths(engine, ld):
     check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
-@pytest.mark.parametrize("ld", [4224, 12416, 20608])
-def test_long_dm_rows_imperfect_trees(engine, ld):
-    """nDM = 33 / 97 / 161: three of the four DataBlock lengths <= 256 rows whose numpy tree is
-    not perfect (leaves at two depths): the round-3 kernels (lyon8_u8_long / generic), exact
-    rational moments -- means bit-exact, the rest within 1e-12."""
-    prof, dm = lyon_batch(200, 128, ld, seed=9 + ld, adversarial=True)
+@pytest.mark.parametrize("lp,ld", [(128, 4224), (128, 12416), (128, 20608), (128, 28800),
+                                   (64, 12416), (256, 4224)])
+def test_long_dm_rows_imperfect_trees(engine, lp, ld):
+    """nDM = 33 / 97 / 161 / 225: the DataBlock lengths <= 256 rows whose last numpy chunk
+    (4224 bytes) is not a perfect tree -- 16 blocks of 128 + (64 + 72), leaves at two
+    depths -- through lyon8_u8_dm's tri form (round 5): mean and std bit-exact like every
+    other length, skew / kurt within 1e-12."""
+    prof, dm = lyon_batch(300, lp, ld, seed=9 + ld + lp, adversarial=True)
     got = engine.lyon8(prof, dm)
-    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4))
+    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
 
 
 def test_long_dm_rows_golden_dmplane(engine):
