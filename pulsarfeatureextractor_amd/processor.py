@@ -44,12 +44,14 @@ PFD_RES = ("*.pfd", "*.pfd.36scrunch")
 
 
 def discover(directory: str, regexes) -> list[str]:
-    """os.walk + fnmatch in the reference's order (:491-497)."""
+    """os.walk + fnmatch in the reference's order (:491-497).  os.path.join(root, fn) of a
+    listed name is root + "/" + fn (root + fn when root ends in "/"): the same strings,
+    built without a call per file (half of the discovery time of a 500k-file directory)."""
     out = []
     for ft in regexes:
         for root, _subs, filenames in os.walk(directory):
-            for fn in fnmatch.filter(filenames, ft):
-                out.append(os.path.join(root, fn))
+            pre = root if root.endswith("/") or not root else root + "/"
+            out.extend([pre + fn for fn in fnmatch.filter(filenames, ft)])
     return out
 
 
@@ -490,6 +492,14 @@ class DataProcessor:
 
     # ---- discovery ---------------------------------------------------------------
     def _candidates(self, directory, regexes, single):
+        t0 = time.perf_counter()
+        try:
+            return self._candidates_(directory, regexes, single)
+        finally:
+            if self._run is not None:
+                self._run.add("discover", time.perf_counter() - t0)
+
+    def _candidates_(self, directory, regexes, single):
         if directory == "":
             directory = os.path.dirname(os.path.realpath(__file__))
         if not single:
@@ -809,6 +819,7 @@ class DataProcessor:
         start = datetime.datetime.now()
         mode = "profile" if genProfileData else "scores"
         run = RunMetrics(mode, self.start)
+        self._run = run
         paths = self._candidates(directory, regexes, single)
         ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0, run)
         self._summary(len(paths), ok, failed, start, run=run)
@@ -836,6 +847,7 @@ class DataProcessor:
         self.verbose = bool(verbose)
         start = datetime.datetime.now()
         run = RunMetrics("separately", self.start)
+        self._run = run
         paths = self._candidates(directory, regexes, single)
 
         from ._native import format_rows
@@ -873,6 +885,7 @@ class DataProcessor:
             writers.write_arff_header(outPath, writers.arff_header("dmprof"))
         start = datetime.datetime.now()
         run = RunMetrics("lyon8", self.start)
+        self._run = run
         paths = self._candidates(directory, regexes, single)
         ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0, run)
         self._summary(len(paths), ok, failed, start, run=run)
@@ -920,6 +933,7 @@ class DataProcessor:
                  "dm": directory + "/DMCurve.csv"}
         start = datetime.datetime.now()
         run = RunMetrics("label", self.start)
+        self._run = run
         paths = self._candidates(directory, regexes, False)
         lab = "0"
         out = {k: [] for k in ("scores", "profile", "dm", "meta")}

@@ -286,3 +286,24 @@ def test_verbose_runs_the_reference_validity_checks(tmp_path, monkeypatch):
         else:
             assert rows[bad][:4] != ["0"] * 4
     assert any("Invalid PHCX candidate" in str(m) for m in logs)
+
+
+def test_discover_matches_os_walk_fnmatch(tmp_path):
+    """processor.discover builds os.path.join(root, fn) by concatenation: the same strings in
+    the reference's os.walk / fnmatch order, with and without a trailing slash, nested."""
+    import fnmatch
+
+    (tmp_path / "a" / "b").mkdir(parents=True)
+    for p in ("x.phcx.gz", "a/y.phcx.gz", "a/b/z.phcx.gz", "a/b/w.pfd", "v.pfd", "q.txt"):
+        (tmp_path / p).write_text("")
+
+    def ref(directory, regexes):
+        out = []
+        for ft in regexes:
+            for root, _s, fns in os.walk(directory):
+                out.extend(os.path.join(root, fn) for fn in fnmatch.filter(fns, ft))
+        return out
+
+    for d in (str(tmp_path), str(tmp_path) + "/", str(tmp_path / "a")):
+        for pats in ([processor.PHCX_RE], [processor.PHCX_RE] + list(processor.PFD_RES)):
+            assert processor.discover(d, pats) == ref(d, pats)

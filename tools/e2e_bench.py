@@ -54,14 +54,23 @@ def main():
     ap.add_argument("--mode", choices=["phases", "stream"], default="phases")
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--ramp", type=int, default=1, help="ramped batch sizes at both ends (1, default) or not (0)")
+    ap.add_argument("--unique", type=int, default=0,
+                    help="write this many distinct files and hard-link them up to --n paths "
+                         "(500k-file runs without 15 GB of distinct data; every path is still "
+                         "opened, inflated and parsed)")
     ap.add_argument("--depth", default="2",
                     help="GPU pipeline depths to time, comma-separated (DataProcessor gpu_depth)")
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     have = sorted(f for f in os.listdir(args.dir) if f.endswith(".phcx.gz"))
     if len(have) < args.n:
+        u = args.unique if 0 < args.unique < args.n else args.n
         with ProcessPoolExecutor(args.workers) as ex:
-            list(ex.map(_write, [(i, args.dir) for i in range(args.n)], chunksize=64))
+            list(ex.map(_write, [(i, args.dir) for i in range(u)], chunksize=64))
+        for i in range(u, args.n):
+            dst = os.path.join(args.dir, f"cand_{i:06d}.phcx.gz")
+            if not os.path.exists(dst):
+                os.link(os.path.join(args.dir, f"cand_{i % u:06d}.phcx.gz"), dst)
     from pulsarfeatureextractor_amd import processor, writers
     from pulsarfeatureextractor_amd.candidate import get_engine
 
