@@ -773,8 +773,11 @@ def main():
     lp_default = {"subband": 256}.get(args.path, 128)
     lp = args.lp or lp_default
     if args.n is None:
+        # pfd22: 131 072 folds (64 GB of 16x32x128 fp64 folds resident) -- the pooled LM
+        # kernels need ~100 k fits in flight to fill their slots (32 768 folds: 516 k, 65 536:
+        # 669 k, 131 072: 800 k folds/s, profiles/r05_bench_pfd22_batches.txt)
         args.n = {"lyon8": 10_000_000, "bates22": 1_000_000, "subband": 1_000_000,
-                  "all30": 1_000_000, "pfd": 32768, "pfd22": 32768}[args.path]
+                  "all30": 1_000_000, "pfd": 32768, "pfd22": 131072}[args.path]
     if args.cpu_sample is None:
         args.cpu_sample = {"lyon8": 8000, "bates22": 300, "subband": 200, "all30": 300,
                            "pfd": 200, "pfd22": 60}[args.path]
