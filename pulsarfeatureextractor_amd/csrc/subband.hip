@@ -198,6 +198,58 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// acc + v(lane 0) + v(lane 1) + ... + v(lane cnt-1), left to right (a reference loop's order),
+// through a 64-double LDS scratch: every lane reads the same 16 B (a broadcast), so each term
+// costs one v_add_f64 instead of two v_readlane and an add
+__device__ __forceinline__ double fold_lanes(double acc, double v, int cnt, double* scratch) {
+  scratch[lane_id()] = v;
+  wave_lds_sync();
+  int t = 0;
+  for (; t + 2 <= cnt; t += 2) {
+    const double2 p = *reinterpret_cast<const double2*>(scratch + t);
+    acc += p.x;
+    acc += p.y;
+  }
+  if (t < cnt) acc += scratch[t];
+  wave_lds_sync();
+  return acc;
+}
+
+// rms_of_maxbins with band i in lane i % 64 (chunks of 64 bands), the same bits: the means are
+// sums of integers (exact in any order), the two sums of squares are folded in band order, and
+// a band outside |v - med| <= wb adds +0.0 to a non-negative sum, which leaves its bits alone
+__device__ __forceinline__ double rms_of_maxbins_wave(const int* maxbin, int nsub, int wb, double* scratch) {
+  const int lane = lane_id();
+  int isum = 0;
+  for (int i0 = 0; i0 < nsub; i0 += 64) isum += i0 + lane < nsub ? maxbin[i0 + lane] : 0;
+  isum = wsum_i(isum);  // <= 65536 bands x 17 bits: no overflow
+  const double msum = (double)isum;
+  const double med = msum / (double)nsub;
+  int count = 0;
+  double var_med = 0.0;
+  for (int i0 = 0; i0 < nsub; i0 += 64) {
+    const int cnt = nsub - i0 < 64 ? nsub - i0 : 64;
+    const double v = lane < cnt ? (double)maxbin[i0 + lane] : 0.0;
+    const bool in = lane < cnt && fabs(v - med) <= (double)wb;
+    count += __builtin_popcountll(__ballot(in));
+    var_med = fold_lanes(var_med, in ? (v - med) * (v - med) : 0.0, cnt, scratch);
+  }
+  double var;
+  if (count > 1) {
+    var = var_med / (double)(count - 1);
+  } else {
+    const double mu = msum / (double)nsub;
+    var = 0.0;
+    for (int i0 = 0; i0 < nsub; i0 += 64) {
+      const int cnt = nsub - i0 < 64 ? nsub - i0 : 64;
+      const double v = lane < cnt ? (double)maxbin[i0 + lane] : 0.0;
+      var = fold_lanes(var, (v - mu) * (v - mu), cnt, scratch);
+    }
+    var /= (double)(nsub - 1);
+  }
+  return sqrt(var) / (double)wb;
+}
+
 // SL = ceil(lsb / 64) window / bin slots per lane; WPB waves (candidates) per block
 template <int SL, typename PT, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
@@ -391,7 +443,7 @@ __host__ __device__ constexpr int sb_pad16(int nsub) { return (nsub + 15) & ~15;
 template <int LSB>
 __host__ __device__ constexpr size_t fast_wave_lds(int nsub) {
   return ((size_t)sb_pad16(nsub) * sb_stride<uint16_t>(LSB) * 2 + 15) / 16 * 16 +
-         ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16;
+         ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16 + 64 * sizeof(double);
 }
 
 // inclusive scan of x over the SEG-lane segments of a DPP row (SEG <= 16): row_shr reads
@@ -480,6 +532,8 @@ void k_subband_fast(SubArgs a) {
   uint16_t* E = reinterpret_cast<uint16_t*>(wbase);
   int* bstat = reinterpret_cast<int*>(wbase + ((size_t)npad * STRIDE * 2 + 15) / 16 * 16);
   int* maxbin = bstat + 3 * nsub;
+  double* fold = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(bstat) +
+                                           ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16);
 
   const double width = a.scal[c * PFE_NSCAL + PFE_SCAL_WIDTH];
   const double wbd = ceil(width * (double)LSB);                      // :1603
@@ -528,9 +582,25 @@ void k_subband_fast(SubArgs a) {
       const int off = base + 1024 * u + 16 * lane;
       if (base + 1024 * u >= total) break;  // wave-uniform
       const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-      uint32_t e[16];
-      const uint32_t tot = piece_prefix(wv, e);
+      // word prefixes first, then the band offset folded into every v_dot4 accumulator: each
+      // u16 pair is one v_lshl_or (every E of a band is < 2^16 at <= 256 bins, so no carry
+      // crosses the halves)
+      uint32_t run[4];
+      run[0] = 0;
+#pragma unroll
+      for (int d = 1; d < 4; ++d) run[d] = __builtin_amdgcn_udot4(wv[d - 1], 0x01010101u, run[d - 1], false);
+      const uint32_t tot = __builtin_amdgcn_udot4(wv[3], 0x01010101u, run[3], false);
       const uint32_t excl = seg_scan_incl<SEG>(tot, pos) - tot;
+      uint32_t pk[8];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t e0 = excl + run[d];
+        const uint32_t e1 = __builtin_amdgcn_udot4(wv[d], 0x00000001u, e0, false);
+        const uint32_t e2 = __builtin_amdgcn_udot4(wv[d], 0x00000101u, e0, false);
+        const uint32_t e3 = __builtin_amdgcn_udot4(wv[d], 0x00010101u, e0, false);
+        pk[2 * d] = e0 | (e1 << 16);
+        pk[2 * d + 1] = e2 | (e3 << 16);
+      }
       int X2 = 0, XP = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -542,9 +612,6 @@ void k_subband_fast(SubArgs a) {
       if (off < total) {
         const int band = off / LSB;
         uint16_t* row = E + band * STRIDE + 16 * pos;
-        uint32_t pk[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) pk[t] = ((e[2 * t] + excl) & 0xFFFFu) | ((e[2 * t + 1] + excl) << 16);
         reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
         reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
         if (pos == SEG - 1) {
@@ -572,8 +639,7 @@ void k_subband_fast(SubArgs a) {
       const double cc = fabs(sb_corr(d * inv2, q2 * inv2, pvar * inv2));
       v = cc > 0.0055 ? cc : 0.0;  // adding 0.0 leaves the running sum's bits unchanged
     }
-    const int cnt = nsub - i0 < 64 ? nsub - i0 : 64;
-    for (int t = 0; t < cnt; ++t) integ += bcast(v, t);
+    integ = fold_lanes(integ, v, nsub - i0 < 64 ? nsub - i0 : 64, fold);
   }
 
   // ---- s20 / s21 over blocks of 16 bands --------------------------------------------------
@@ -654,7 +720,7 @@ void k_subband_fast(SubArgs a) {
   }
   const double mean_corr = (0.5 * (zs - (double)valid)) / (double)m;
   wave_lds_sync();
-  const double rms = rms_of_maxbins(maxbin, nsub, wb);
+  const double rms = rms_of_maxbins_wave(maxbin, nsub, wb, fold);
   if (lane == 0) {
     double* o = a.out + c * a.ldo;
     o[0] = rms;
