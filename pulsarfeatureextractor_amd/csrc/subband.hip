@@ -440,9 +440,15 @@ __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
 //     is 0 by construction and its key (0 << 10 | 1023 - j) loses to every real window
 //     (those have smaller j).
 __host__ __device__ constexpr int sb_pad16(int nsub) { return (nsub + 15) & ~15; }
+// the fast kernel's u16 row pitch: lsb + 1 prefixes and a zero tail to lsb + 31 (read by the
+// band-per-lane pass past the last window), 16-B aligned rows, and a pitch of 4 x odd dwords so
+// that the 16 bands of a block read by one row of lanes land in 16 distinct bank groups
+__host__ __device__ constexpr int sb_stride_fast(int lsb) {
+  return ((lsb + 32 + 15) & ~15) + 8;  // = 8 (mod 16)
+}
 template <int LSB>
 __host__ __device__ constexpr size_t fast_wave_lds(int nsub) {
-  return ((size_t)sb_pad16(nsub) * sb_stride<uint16_t>(LSB) * 2 + 15) / 16 * 16 +
+  return ((size_t)sb_pad16(nsub) * sb_stride_fast(LSB) * 2 + 15) / 16 * 16 +
          ((size_t)nsub * 4 * sizeof(int) + 15) / 16 * 16 + 64 * sizeof(double);
 }
 
@@ -507,6 +513,33 @@ __device__ __forceinline__ void reduce_scatter16(T (&v)[16], int lane, Op op) {
   v[0] = op(v[0], xor_v<16>(v[0]));
   v[0] = op(v[0], xor_v<32>(v[0]));
 }
+// The same reduce-scatter with every in-row exchange on DPP (no ds_bpermute): the partners
+// are i^15 (row_mirror), i^7 (row_half_mirror), i^3 and i^1 (quad_perm), each differing from
+// the lane in the bit its step splits on and agreeing in the bits earlier steps split on, so
+// after the four steps each lane of a row has summed all 16 lanes; lane l holds entry l & 15
+template <int CTRL>
+__device__ __forceinline__ int dpp_x(int v) { return dpp_i32<CTRL>(v); }
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_x(unsigned long long v) { return dpp_u64<CTRL>(v); }
+template <int M, int H, int CTRL, typename T, typename Op>
+__device__ __forceinline__ void rs_step_dpp(T (&v)[16], int lane, Op op) {
+  const bool hi = (lane & M) != 0;
+#pragma unroll
+  for (int t = 0; t < H; ++t) {
+    const T keep = hi ? v[t + H] : v[t];
+    const T send = hi ? v[t] : v[t + H];
+    v[t] = op(keep, dpp_x<CTRL>(send));
+  }
+}
+template <typename T, typename Op>
+__device__ __forceinline__ void reduce_scatter16_dpp(T (&v)[16], int lane, Op op) {
+  rs_step_dpp<8, 8, DPP_ROW_MIRROR>(v, lane, op);
+  rs_step_dpp<4, 4, DPP_ROW_HALF_MIRROR>(v, lane, op);
+  rs_step_dpp<2, 2, 0x1B>(v, lane, op);  // quad_perm [3,2,1,0]
+  rs_step_dpp<1, 1, DPP_QUAD_XOR1>(v, lane, op);
+  v[0] = op(v[0], xor_v<16>(v[0]));
+  v[0] = op(v[0], xor_v<32>(v[0]));
+}
 __device__ __forceinline__ int bitrev4(int l) {
   return ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
 }
@@ -519,7 +552,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PFE_SU
 void k_subband_fast(SubArgs a) {
   constexpr int SL = LSB >= 64 ? LSB / 64 : 1;  // window slots per lane
   constexpr int SEG = LSB / 16;                 // lanes per band in the 16-byte piece layout
-  constexpr int STRIDE = sb_stride<uint16_t>(LSB);
+  constexpr int STRIDE = sb_stride_fast(LSB);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   extern __shared__ __align__(16) unsigned char sb_lds[];
   const int lane = lane_id();
@@ -582,25 +615,27 @@ void k_subband_fast(SubArgs a) {
       const int off = base + 1024 * u + 16 * lane;
       if (base + 1024 * u >= total) break;  // wave-uniform
       const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-      // word prefixes first, then the band offset folded into every v_dot4 accumulator: each
-      // u16 pair is one v_lshl_or (every E of a band is < 2^16 at <= 256 bins, so no carry
-      // crosses the halves)
-      uint32_t run[4];
-      run[0] = 0;
+      // the piece total first, then the 16 prefixes as one running chain of byte adds from
+      // the band offset (a v_dot4 issues at about a quarter of the rate of an add on gfx950,
+      // profiles/r04_ubench_op_rates.txt); each u16 pair is one v_lshl_or (every E of a band
+      // is < 2^16 at <= 256 bins, so no carry crosses the halves)
+      uint32_t tot = 0;
 #pragma unroll
-      for (int d = 1; d < 4; ++d) run[d] = __builtin_amdgcn_udot4(wv[d - 1], 0x01010101u, run[d - 1], false);
-      const uint32_t tot = __builtin_amdgcn_udot4(wv[3], 0x01010101u, run[3], false);
-      const uint32_t excl = seg_scan_incl<SEG>(tot, pos) - tot;
+      for (int d = 0; d < 4; ++d) tot = __builtin_amdgcn_sad_u8(wv[d], 0u, tot);
+      uint32_t e = seg_scan_incl<SEG>(tot, pos) - tot;
       uint32_t pk[8];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const uint32_t e0 = excl + run[d];
-        const uint32_t e1 = __builtin_amdgcn_udot4(wv[d], 0x00000001u, e0, false);
-        const uint32_t e2 = __builtin_amdgcn_udot4(wv[d], 0x00000101u, e0, false);
-        const uint32_t e3 = __builtin_amdgcn_udot4(wv[d], 0x00010101u, e0, false);
+        const uint32_t x = wv[d];
+        const uint32_t e0 = e;
+        const uint32_t e1 = e0 + (x & 0xFFu);
+        const uint32_t e2 = e1 + ((x >> 8) & 0xFFu);
+        const uint32_t e3 = e2 + ((x >> 16) & 0xFFu);
+        e = e3 + (x >> 24);
         pk[2 * d] = e0 | (e1 << 16);
         pk[2 * d + 1] = e2 | (e3 << 16);
       }
+      const uint32_t excl = e - tot;
       int X2 = 0, XP = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -615,7 +650,11 @@ void k_subband_fast(SubArgs a) {
         reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
         reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
         if (pos == SEG - 1) {
-          row[16] = (uint16_t)(excl + tot);                        // E[band][LSB] = T
+          // E[band][LSB] = T, then the zero tail E[band][LSB + 1 .. LSB + 31]
+          reinterpret_cast<u32x4*>(row + 16)[0] = (u32x4){excl + tot, 0, 0, 0};
+          reinterpret_cast<u32x4*>(row + 16)[1] = (u32x4){0, 0, 0, 0};
+          reinterpret_cast<u32x4*>(row + 16)[2] = (u32x4){0, 0, 0, 0};
+          reinterpret_cast<u32x4*>(row + 16)[3] = (u32x4){0, 0, 0, 0};
           bstat[3 * band + 0] = (int)(excl + tot);
           bstat[3 * band + 1] = X2;
           bstat[3 * band + 2] = XP;
@@ -649,61 +688,86 @@ void k_subband_fast(SubArgs a) {
   for (int k = 0; k < SL; ++k) W[k] = 0.0;
   double C = 0.0;
   int valid = 0;
-  // per window slot, band-independent: the prefix indices (a window past the last one reads
-  // E[lo] twice: b = 0) and the low half of the maximum key
-  int lo_k[SL], hi_k[SL], jk[SL];
+  // pass 2's window slots (lane = window): the prefix indices, band-independent (a window
+  // past the last one reads E[lo] twice: b = 0)
+  int lo_k[SL], hi_k[SL];
 #pragma unroll
   for (int k = 0; k < SL; ++k) {
     const int j = lane + 64 * k;
     lo_k[k] = j < LSB ? j : LSB;
     hi_k[k] = j < nw ? j + wb : lo_k[k];
-    jk[k] = 1023 - j;
   }
+  // pass 1's layout (lane = band): band bi of the block, windows j = qtr + 4t, t < T; the
+  // steps run in chunks of 8 (skipped past T), and a window j >= nw of the last chunk reads
+  // E[j + wb] from the zero tail of its row (indices lsb + 1 .. lsb + 31), so its saturated
+  // difference is 0: no masks
+  const int bi = lane & 15, qtr = lane >> 4;
+  const int T = (nw + 3) >> 2;
+  constexpr int NCH = (LSB / 4 + 7) / 8;
   for (int blk = 0; blk < nsub; blk += SB_NB) {
     const int nb = nsub - blk < SB_NB ? nsub - blk : SB_NB;
-    int bv[SB_NB][SL];
-    int sA[SB_NB], kA[SB_NB];
-    unsigned long long qA[SB_NB];
     const uint16_t* rows = E + blk * STRIDE;  // bands past nsub are the zero rows
+    // ---- pass 1: S = sum b, sum b^2 and the first maximum of each band -------------------
+    const uint16_t* plo = rows + bi * STRIDE + qtr;
+    const uint16_t* phi = plo + wb;
+    int sv = 0, kl = 0;
+    unsigned long long qv = 0;
 #pragma unroll
-    for (int ii = 0; ii < SB_NB; ++ii) {
-      int sv = 0, kmax = 0;
-      unsigned long long qv = 0;
-      const uint16_t* row = rows + ii * STRIDE;
+    for (int ch = 0; ch < NCH; ++ch) {
+      if (8 * ch < T) {  // wave-uniform
 #pragma unroll
-      for (int k = 0; k < SL; ++k) {
-        const int b = (int)row[hi_k[k]] - (int)row[lo_k[k]];
-        const int kk = (b << 10) | jk[k];
-        kmax = kk > kmax ? kk : kmax;
-        bv[ii][k] = b;
-        sv += b;
-        // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int, so
-        // the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
-        qv += (uint32_t)__umul24((uint32_t)b, (uint32_t)b);
+        for (int u = 0; u < 8; ++u) {
+          const int t = 8 * ch + u;
+          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[4 * t], (uint32_t)plo[4 * t]);
+          // the lane's own key: ties go to the smaller t (the smaller j of this lane)
+          const int kk = (int)((b << 6) | (uint32_t)(63 - t));
+          kl = kk > kl ? kk : kl;
+          sv += (int)b;
+          // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
+          // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
+          qv += (uint32_t)__umul24(b, b);
+        }
       }
-      sA[ii] = sv;
-      qA[ii] = qv;
-      kA[ii] = kmax;
     }
-    reduce_scatter16(sA, lane, [](int x, int y) { return x + y; });
-    reduce_scatter16(qA, lane, [](unsigned long long x, unsigned long long y) { return x + y; });
-    reduce_scatter16(kA, lane, [](int x, int y) { return x > y ? x : y; });
-    // lane l (< 16) now holds band bitrev4(l) of the block
-    const int beta = bitrev4(lane & 15);
-    const bool inb = beta < nb;
-    const long long N = (long long)nw * (long long)qA[0] - (long long)sA[0] * sA[0];
+    // the lane's best window as the band-wide key (b << 10) | (1023 - j), then the band's four
+    // quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums and a maximum
+    int key = ((kl >> 6) << 10) | (1023 - (qtr + 4 * (63 - (kl & 63))));
+    sv += __shfl_xor(sv, 16);
+    qv += xor_u64<16>(qv);
+    key = max(key, __shfl_xor(key, 16));
+    sv += __shfl_xor(sv, 32);
+    qv += xor_u64<32>(qv);
+    key = max(key, __shfl_xor(key, 32));
+    const bool inb = bi < nb;
+    const long long N = (long long)nw * (long long)qv - (long long)sv * sv;
     const bool ok = inb && N > 0;
     const double rl = ok ? 1.0 / sqrt(dnw * (double)N) : 0.0;
-    const double cl = (double)sA[0] * rl;
-    if (lane < 16 && inb) maxbin[blk + beta] = 1023 - (kA[0] & 1023) + wb / 2;  // :1628
+    const double cl = (double)sv * rl;
+    if (lane < 16 && inb) maxbin[blk + bi] = 1023 - (key & 1023) + wb / 2;  // :1628
     valid += __builtin_popcountll(__ballot(lane < 16 && ok));
-#pragma unroll
-    for (int ii = 0; ii < SB_NB; ++ii) {
-      const double r = bcast(rl, bitrev4(ii));
-      C += bcast(cl, bitrev4(ii));
-#pragma unroll
-      for (int k = 0; k < SL; ++k) W[k] = __builtin_fma(r, (double)bv[ii][k], W[k]);
+    // ---- pass 2: W_j += r_i b_ij in band order (the 16 bands' r and S r through LDS,
+    // broadcast reads; C summed in band order) ---------------------------------------------
+    if (lane < 16) {
+      fold[bi] = rl;
+      fold[16 + bi] = cl;
     }
+    wave_lds_sync();
+#pragma unroll
+    for (int ii = 0; ii < SB_NB; ii += 2) {
+      const double2 r2 = *reinterpret_cast<const double2*>(fold + ii);
+      const double2 c2 = *reinterpret_cast<const double2*>(fold + 16 + ii);
+      C += c2.x;
+      C += c2.y;
+      const uint16_t* row0 = rows + ii * STRIDE;
+      const uint16_t* row1 = row0 + STRIDE;
+#pragma unroll
+      for (int k = 0; k < SL; ++k)
+        W[k] = __builtin_fma(r2.x, (double)((int)row0[hi_k[k]] - (int)row0[lo_k[k]]), W[k]);
+#pragma unroll
+      for (int k = 0; k < SL; ++k)
+        W[k] = __builtin_fma(r2.y, (double)((int)row1[hi_k[k]] - (int)row1[lo_k[k]]), W[k]);
+    }
+    wave_lds_sync();
   }
   // s21: sum_{i<k} cc_ik = (sum_j Z_j^2 - v) / 2 with Z_j = nw W_j - C, |z_i|^2 = 1
   double zs = 0.0;

@@ -43,16 +43,91 @@ SUPERB_RE = "*.phcx"
 PFD_RES = ("*.pfd", "*.pfd.36scrunch")
 
 
-def discover(directory: str, regexes) -> list[str]:
-    """os.walk + fnmatch in the reference's order (:491-497).  os.path.join(root, fn) of a
-    listed name is root + "/" + fn (root + fn when root ends in "/"): the same strings,
-    built without a call per file (half of the discovery time of a 500k-file directory)."""
-    out = []
+def iter_discover(directory: str, regexes):
+    """os.walk + fnmatch in the reference's order (:491-497), one list of paths per directory
+    and pattern.  os.path.join(root, fn) of a listed name is root + "/" + fn (root + fn when
+    root ends in "/"): the same strings, built without a call per file (half of the discovery
+    time of a 500k-file directory)."""
     for ft in regexes:
         for root, _subs, filenames in os.walk(directory):
             pre = root if root.endswith("/") or not root else root + "/"
-            out.extend([pre + fn for fn in fnmatch.filter(filenames, ft)])
+            hit = [pre + fn for fn in fnmatch.filter(filenames, ft)]
+            if hit:
+                yield hit
+
+
+def discover(directory: str, regexes) -> list[str]:
+    out = []
+    for hit in iter_discover(directory, regexes):
+        out.extend(hit)
     return out
+
+
+class PathFeed:
+    """The discovered candidate paths of a run, filled by a background walk (iter_discover's
+    order, the first `skip` dropped) while the first batches are already parsed: _stream
+    takes a batch as soon as its paths are listed, so the walk of a large directory overlaps
+    the parsing instead of preceding it.  Reads block until the paths they need are listed;
+    len() waits for the whole walk.  on_done(total, skipped) runs on the walk thread."""
+
+    def __init__(self, gen=None, skip=0, on_done=None, paths=None):
+        self._paths = list(paths) if paths is not None else []
+        self._done = gen is None
+        self._err = None
+        self._cv = threading.Condition()
+        if gen is not None:
+            threading.Thread(target=self._walk, args=(gen, int(skip), on_done), daemon=True).start()
+
+    def _walk(self, gen, skip, on_done):
+        seen = 0
+        try:
+            for hit in gen:
+                if seen + len(hit) <= skip:
+                    seen += len(hit)
+                    continue
+                hit = hit[max(0, skip - seen):]
+                seen = max(seen, skip) + len(hit)
+                with self._cv:
+                    self._paths.extend(hit)
+                    self._cv.notify_all()
+        except BaseException as e:  # re-raised to the reader
+            self._err = e
+        finally:
+            with self._cv:
+                self._done = True
+                self._cv.notify_all()
+        if on_done is not None and self._err is None:
+            on_done(seen, min(seen, skip))
+
+    def wait(self, n):
+        """Block until n paths are listed or the walk is over; -> the number listed (<= n)."""
+        with self._cv:
+            self._cv.wait_for(lambda: self._done or len(self._paths) >= n)
+            if self._err is not None:
+                raise self._err
+            return min(n, len(self._paths))
+
+    def known_total(self):
+        with self._cv:
+            return len(self._paths) if self._done else None
+
+    def __len__(self):
+        with self._cv:
+            self._cv.wait_for(lambda: self._done)
+        if self._err is not None:
+            raise self._err
+        return len(self._paths)
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            stop = len(self) if k.stop is None else k.stop
+            self.wait(stop)
+        else:
+            self.wait(k + 1)
+        return self._paths[k]
+
+    def __iter__(self):
+        return iter(self[:])
 
 
 def _parse_one(path):
@@ -249,20 +324,67 @@ def _cuts(n, batch, ramp=True):
     return [0] + np.cumsum(sizes).tolist()
 
 
+def _tail_cuts(lo, n, batch, ramp=True):
+    """The rest of _cuts once the total n is known at offset lo: full batches, then the
+    closing batch/2, batch/4, batch/8 when the remainder is long enough."""
+    steps = [batch // 8, batch // 4, batch // 2]
+    rem = n - lo
+    if rem <= 0:
+        return []
+    if not ramp or batch < 64 or rem < sum(steps) + batch:
+        return list(range(lo + batch, n, batch)) + [n]
+    sizes = []
+    r = rem - sum(steps)
+    while r > 0:
+        sizes.append(min(batch, r))
+        r -= sizes[-1]
+    sizes += steps[::-1]
+    return (lo + np.cumsum(sizes)).tolist()
+
+
+class _Cuts:
+    """Batch boundaries over a PathFeed: _cuts(n) when the total is known up front; while the
+    walk is still listing, the opening batch/8, batch/4, batch/2 and then full batches, each
+    taken once its paths are listed, and _tail_cuts from wherever the walk ends."""
+
+    def __init__(self, feed, batch, ramp):
+        self.feed, self.batch, self.ramp = feed, batch, ramp
+        n = feed.known_total()
+        self.cuts = _cuts(n, batch, ramp) if n else [0]
+        self.final = n is not None
+
+    def has(self, k):
+        """Is there a batch k (cuts[k]..cuts[k + 1])?  Blocks until that is known."""
+        while len(self.cuts) <= k + 1 and not self.final:
+            lo = self.cuts[-1]
+            nb = len(self.cuts) - 1
+            steps = [self.batch // 8, self.batch // 4, self.batch // 2]
+            size = steps[nb] if self.ramp and self.batch >= 64 and nb < 3 else self.batch
+            got = self.feed.wait(lo + size + 1)  # one more: is this the last batch?
+            n = self.feed.known_total()
+            if n is not None:
+                self.cuts += _tail_cuts(lo, n, self.batch, self.ramp)
+                self.final = True
+            elif got > lo + size:
+                self.cuts.append(lo + size)
+        return len(self.cuts) > k + 1
+
+
 def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3, ramp=True):
     """parse(batch paths) on a helper thread, up to `ahead` batches beyond those being scored
     (the parser never waits for a GPU step unless it is that far ahead); score(parsed, slot)
     of batch k on slot k % depth (one thread per slot, so up to `depth` batches are scored at
     once, each on its own engine handle and pinned slabs); emit(batch offset, batch paths,
     results) on the calling thread in discovery order, overlapping the next batches'
-    scoring."""
-    if not paths:
+    scoring.  `paths` is a list or a PathFeed still being filled by its walk."""
+    feed = paths if isinstance(paths, PathFeed) else PathFeed(paths=paths)
+    cut = _Cuts(feed, batch, ramp)
+    if not cut.has(0):
         return
-    cuts = _cuts(len(paths), batch, ramp)
-    nb = len(cuts) - 1
+    cuts = cut.cuts
 
     def part(k):
-        return paths[cuts[k]:cuts[k + 1]]
+        return feed[cuts[k]:cuts[k + 1]]
 
     slots = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]
     try:
@@ -270,24 +392,26 @@ def _stream(paths, parse, score, emit, batch=BATCH, depth=1, ahead=3, ramp=True)
             parsed, scored = {}, {}
 
             def submit_parse(k):
-                if k < nb and k not in parsed and k not in scored:
+                if k not in parsed and k not in scored and cut.has(k):
                     parsed[k] = px.submit(parse, part(k))
 
             def submit_score(k):
-                if k < nb and k not in scored:
+                if k not in scored and cut.has(k):
                     submit_parse(k)
                     f = parsed.pop(k)
                     scored[k] = slots[k % depth].submit(lambda f=f, k=k: score(f.result(), k % depth))
 
-            for k in range(min(depth + ahead, nb)):
+            for k in range(depth + ahead):
                 submit_parse(k)
-            for k in range(min(depth, nb)):
+            for k in range(depth):
                 submit_score(k)
-            for k in range(nb):
+            k = 0
+            while cut.has(k):
                 res = scored.pop(k).result()
                 submit_score(k + depth)
                 submit_parse(k + depth + ahead)
                 emit(cuts[k], part(k), res)
+                k += 1
     finally:
         for ex in slots:
             ex.shutdown(wait=True)
@@ -492,19 +616,29 @@ class DataProcessor:
 
     # ---- discovery ---------------------------------------------------------------
     def _candidates(self, directory, regexes, single):
+        """The run's candidate paths: a PathFeed whose walk runs beside the first batches'
+        parsing for a directory, a list otherwise.  Run metrics "discover": the walk's time."""
         t0 = time.perf_counter()
+        if directory == "":
+            directory = os.path.dirname(os.path.realpath(__file__))
+        if not single:
+            run = self._run
+
+            def done(total, skipped):
+                if run is not None:
+                    run.add("discover", time.perf_counter() - t0)
+                if self.start:
+                    self.log(f"Resuming after the first {skipped} of {total} candidates")
+
+            return PathFeed(iter_discover(directory, regexes), skip=self.start, on_done=done)
         try:
-            return self._candidates_(directory, regexes, single)
+            return self._candidates_(directory, regexes)
         finally:
             if self._run is not None:
                 self._run.add("discover", time.perf_counter() - t0)
 
-    def _candidates_(self, directory, regexes, single):
-        if directory == "":
-            directory = os.path.dirname(os.path.realpath(__file__))
-        if not single:
-            paths = discover(directory, regexes)
-        elif ".txt" in directory:  # a list of candidate paths (the reference reads self.path)
+    def _candidates_(self, directory, regexes):
+        if ".txt" in directory:  # a list of candidate paths (the reference reads self.path)
             with open(directory) as f:
                 paths = [ln.strip() for ln in f if ln.strip()]
         else:

@@ -307,3 +307,51 @@ def test_discover_matches_os_walk_fnmatch(tmp_path):
     for d in (str(tmp_path), str(tmp_path) + "/", str(tmp_path / "a")):
         for pats in ([processor.PHCX_RE], [processor.PHCX_RE] + list(processor.PFD_RES)):
             assert processor.discover(d, pats) == ref(d, pats)
+
+
+def test_stream_over_a_path_feed_still_being_walked():
+    """A directory's paths come from a PathFeed whose walk runs beside the first batches:
+    every path is emitted once, in order, with the same offsets as over the finished list;
+    the batches open with batch/8, /4, /2 while the walk is still listing and close with
+    /2, /4, /8 once it has ended; `skip` drops the first paths; a walk error reaches the
+    reader."""
+    import time as _time
+
+    from pulsarfeatureextractor_amd.processor import PathFeed, _stream
+
+    names = [f"d{i // 97}/f{i}.phcx.gz" for i in range(3000)]
+
+    def slow_walk():
+        for i in range(0, len(names), 97):
+            _time.sleep(0.001)
+            yield names[i:i + 97]
+
+    def parse(part):  # slower than the walk, as parsing a file is than listing it
+        _time.sleep(0.01)
+        return list(part)
+
+    for skip in (0, 250):
+        got, sizes = [], []
+
+        def emit(off, part, res, got=got, sizes=sizes):
+            assert res == ("scored", len(part)) and off == len(got)
+            got.extend(part)
+            sizes.append(len(part))
+
+        feed = PathFeed(slow_walk(), skip=skip)
+        _stream(feed, parse, lambda parsed, slot: ("scored", len(parsed)), emit, batch=128, depth=2)
+        assert got == names[skip:] and len(feed) == len(names) - skip
+        assert sizes[:3] == [16, 32, 64] and sizes[-3:] == [64, 32, 16] and max(sizes) == 128
+
+    done = []
+    feed = PathFeed(iter([names[:10], names[10:20]]), skip=15, on_done=lambda t, s: done.append((t, s)))
+    assert feed[:] == names[15:20] and done == [(20, 15)]
+
+    def broken():
+        yield names[:5]
+        raise OSError("walk failed")
+
+    with pytest.raises(OSError):
+        len(PathFeed(broken()))
+    assert len(PathFeed(iter([]))) == 0
+    _stream(PathFeed(iter([])), None, None, None)  # nothing listed: no batch, no call

@@ -170,6 +170,36 @@ __global__ __launch_bounds__(256) void k_rowsU(const unsigned char* a, const uns
   }
 }
 
+// shape 5b: the same mapping with only one side of the traffic: MODE 1 reads the 256 B of a
+// candidate and stores nothing (the result escapes through an impossible branch), MODE 2
+// stores the 64 B of a candidate and reads nothing -- the read and write parts of the
+// Lyon-8 kernel's traffic, timed apart
+template <int MODE, int U>
+__global__ __launch_bounds__(256) void k_rows_half(const unsigned char* a, const unsigned char* b,
+                                                   double* o, long n) {
+  const int lane = threadIdx.x & 63, sub = lane & 3, cw = lane >> 2;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  u32x4 acc = {0, 0, 0, 0};
+  for (long base = wave * 16 * U; base < n; base += nw * 16 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      long c = base + u * 16 + cw;
+      c = c < n ? c : n - 1;
+      if constexpr (MODE == 1) {
+        const u32x4* pa = (const u32x4*)(a + c * 128 + sub * 32);
+        const u32x4* pb = (const u32x4*)(b + c * 128 + sub * 32);
+        acc ^= __builtin_nontemporal_load(pa) ^ __builtin_nontemporal_load(pa + 1) ^
+               __builtin_nontemporal_load(pb) ^ __builtin_nontemporal_load(pb + 1);
+      } else {
+        f64x2 v = {(double)(c + sub), (double)c};
+        __builtin_nontemporal_store(v, (f64x2*)(o + c * 8 + sub * 2));
+      }
+    }
+  }
+  if (MODE == 1 && acc.x == 0x12345678u && acc.y == 0x9abcdef0u) o[0] = (double)acc.z;
+}
+
 // shape 6: plain float4 copy (calibration against MI355X_MICROARCH.md's 6.29 TB/s)
 __global__ __launch_bounds__(256) void k_copy(const u32x4* a, u32x4* o, long n16) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -233,6 +263,14 @@ int main(int argc, char** argv) {
     ms /= reps;
     printf("%-28s %8.4f ms  %7.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
   };
+  // the Lyon-8 kernel's traffic split: read side alone, write side alone, both (grid 16384
+  // as lyon8_u8_fast3's cap; GB/s over the 320 B of a candidate in every line)
+  for (int rep = 0; rep < 2; ++rep) {
+    run("split: read 256 B only g16384", [&] { hipLaunchKernelGGL((k_rows_half<1, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: write 64 B only g16384", [&] { hipLaunchKernelGGL((k_rows_half<2, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write g16384", [&] { hipLaunchKernelGGL((k_rowsU<1, 1, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("copy (3.2GB moved) g16384", [&] { hipLaunchKernelGGL(k_copy, dim3(16384), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n * 10); });
+  }
   for (int rep = 0; rep < 2; ++rep)
   for (int grid : {1024, 2048}) {
     char nm[64];

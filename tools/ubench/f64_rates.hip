@@ -1,6 +1,7 @@
 // Microbenchmark: issue rates of the instructions the DataBlock kernel is made of, on
 // gfx950 -- independent v_fma_f64 / v_mul_f64 / v_add_f64 streams, a dependent v_add_f64
-// chain, and ds_read_u8 -- per SIMD at 1, 2, 4 and 8 waves per SIMD.
+// chain, the integer ops of the sub-band kernel, and ds_read_u8 -- per SIMD at 1, 2, 4 and 8
+// waves per SIMD (check the op's ISA with --save-temps: the count per element is assumed).
 //   hipcc --offload-arch=gfx950 -O3 -o f64_rates f64_rates.hip && ./f64_rates
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -42,6 +43,45 @@ __global__ __launch_bounds__(256) void k_valu(double* out, double s) {
         u2 v = __builtin_bit_cast(u2, a[j]);
         v.x = __builtin_amdgcn_udot2(__builtin_bit_cast(s2, v.y), __builtin_bit_cast(s2, v.y), v.x, false);
         v.y = __builtin_amdgcn_udot2(__builtin_bit_cast(s2, v.x), __builtin_bit_cast(s2, v.x), v.y, false);
+        a[j] = __builtin_bit_cast(double, v);
+      }
+      if constexpr (OP == 9) {  // v_add_u32 x2 (independent halves)
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        u2 v = __builtin_bit_cast(u2, a[j]);
+        v.x += 0x9e3779b9u; v.y += 0x7f4a7c15u;
+        a[j] = __builtin_bit_cast(double, v);
+      }
+      if constexpr (OP == 10) {  // v_mad_u64_u32 x1
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        unsigned long long u = __builtin_bit_cast(unsigned long long, a[j]);
+        const unsigned b = (unsigned)u;
+        u = (unsigned long long)b * (unsigned)(b >> 3) + u;
+        a[j] = __builtin_bit_cast(double, u);
+      }
+      if constexpr (OP == 11) {  // v_sad_u8 x2
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        u2 v = __builtin_bit_cast(u2, a[j]);
+        v.x = __builtin_amdgcn_sad_u8(v.y, 0u, v.x);
+        v.y = __builtin_amdgcn_sad_u8(v.x, 0u, v.y);
+        a[j] = __builtin_bit_cast(double, v);
+      }
+      if constexpr (OP == 12) {  // v_cvt_f64_i32 x1
+        const int b = (int)__builtin_bit_cast(unsigned long long, a[j]);
+        a[j] = (double)(b ^ 5);
+      }
+      if constexpr (OP == 13) {  // v_add_u32_sdwa (byte-select add) x2
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        u2 v = __builtin_bit_cast(u2, a[j]);
+        v.x = v.x + ((v.y >> 8) & 0xFFu);
+        v.y = v.y + ((v.x >> 16) & 0xFFu);
+        a[j] = __builtin_bit_cast(double, v);
+      }
+      if constexpr (OP == 14) {  // v_cndmask_b32 x2
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        u2 v = __builtin_bit_cast(u2, a[j]);
+        const bool c = (threadIdx.x & 1) != 0;
+        const unsigned x = c ? v.x : v.y, y = c ? v.y : v.x;
+        v.x = x; v.y = y;
         a[j] = __builtin_bit_cast(double, v);
       }
       if constexpr (OP == 8) {  // v_perm_b32 x2
@@ -86,9 +126,13 @@ int main() {
   hipEventCreate(&b);
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const char* names[] = {"v_fma_f64 indep", "v_mul_f64 indep", "v_add_f64 indep", "v_add_f64 dep chain", "u64 add (2 VALU)",
-                         "v_dot4_u32_u8", "v_pk_mul_lo_u16", "v_dot2_u32_u16", "v_perm_b32"};
-  for (int op = 0; op < 9; ++op) {
+  const char* names[] = {"v_fma_f64 indep", "v_mul_f64 indep", "v_add_f64 indep", "v_add_f64 dep chain", "v_lshl_add_u64 (u64 +)",
+                         "v_dot4_u32_u8", "v_pk_mul_lo_u16", "v_dot2_u32_u16", "v_perm_b32",
+                         "v_add_u32", "mad_u64_u32+lshrrev", "v_sad_u8", "v_cvt_f64_i32+xor", "v_add_u32_sdwa", "v_cndmask_b32"};
+  // VALU instructions per element and step, as the gfx950 ISA of each loop has them (the
+  // u64 add is one v_lshl_add_u64; ops 10 and 12 time a pair of different instructions)
+  const int per[] = {1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+  for (int op = 0; op < 15; ++op) {
     for (int wps = 1; wps <= 8; wps *= 2) {
       const int blocks = cus * wps;  // 4 waves per block = one per SIMD
       for (int rep = 0; rep < 2; ++rep) {
@@ -103,6 +147,12 @@ int main() {
           case 6: hipLaunchKernelGGL(k_valu<6>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
           case 7: hipLaunchKernelGGL(k_valu<7>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
           case 8: hipLaunchKernelGGL(k_valu<8>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 9: hipLaunchKernelGGL(k_valu<9>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 10: hipLaunchKernelGGL(k_valu<10>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 11: hipLaunchKernelGGL(k_valu<11>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 12: hipLaunchKernelGGL(k_valu<12>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 13: hipLaunchKernelGGL(k_valu<13>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
+          case 14: hipLaunchKernelGGL(k_valu<14>, dim3(blocks), dim3(256), 0, 0, out, 1.0000001); break;
         }
         hipEventRecord(b);
         hipEventSynchronize(b);
@@ -110,7 +160,7 @@ int main() {
         hipEventElapsedTime(&ms, a, b);
         if (rep == 1) {
           // wave-instructions per SIMD: wps waves x ITERS x 8 (op 4: 2 VALU per element)
-          const double ins = (double)wps * ITERS * 8 * (op >= 4 ? 2 : 1);
+          const double ins = (double)wps * ITERS * 8 * per[op];
           const double cyc = ms * 1e-3 * 2.4e9;
           printf("%-22s waves/SIMD %d: %.2f cycles per wave-instruction per SIMD (at 2.4 GHz)\n",
                  names[op], wps, cyc / ins);
