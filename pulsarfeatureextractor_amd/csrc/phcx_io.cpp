@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <charconv>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -672,8 +673,11 @@ void append_py2_value(std::string& s, double x) {
     s += x > 0 ? "0" : "-0";
     return;
   }
+  // std::to_chars(general, 12) is specified as printf's %.12g in the C locale, and is ~4x
+  // faster than snprintf (the text of 22 scores per line is the largest host cost of a
+  // streamed run after parsing)
   char tmp[40];
-  const int k = std::snprintf(tmp, sizeof tmp, "%.12g", x);
+  const int k = (int)(std::to_chars(tmp, tmp + sizeof tmp, x, std::chars_format::general, 12).ptr - tmp);
   s.append(tmp, (size_t)k);
   if (!std::memchr(tmp, '.', (size_t)k) && !std::memchr(tmp, 'e', (size_t)k)) s += ".0";
 }
