@@ -556,7 +556,8 @@ void k_subband_fast(SubArgs a) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   extern __shared__ __align__(16) unsigned char sb_lds[];
   const int lane = lane_id();
-  const int w = threadIdx.x >> 6;
+  // the wave's candidate, and everything derived from it, in scalar registers
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t c = (int64_t)blockIdx.x * WPB + w;
   if (c >= a.n) return;
   const int nsub = a.nsub;
@@ -574,7 +575,7 @@ void k_subband_fast(SubArgs a) {
     if (lane == 0) atomicOr(&a.status[c], PFE_ST_SUBBAND_FAIL);
     return;
   }
-  const int wb = (int)wbd;
+  const int wb = __builtin_amdgcn_readfirstlane((int)wbd);
   const int nw = LSB - wb + 1;
   const uint8_t* sb = a.sub + c * (int64_t)nsub * LSB;
   const int pos = lane & (SEG - 1);
@@ -582,6 +583,10 @@ void k_subband_fast(SubArgs a) {
   for (int t = nsub * STRIDE / 8 + lane; t < npad * STRIDE / 8; t += 64)
     reinterpret_cast<uint32_t __attribute__((ext_vector_type(4)))*>(E)[t] =
         (uint32_t __attribute__((ext_vector_type(4)))){0, 0, 0, 0};
+  // the zero tails E[band][LSB .. LSB + 31] of the real bands, 64 B each (the prefix pass
+  // then stores E[band][LSB] = T): one 16-B store per lane per 16 bands
+  for (int t = lane; t < nsub * 4; t += 64)
+    reinterpret_cast<u32x4*>(E + (t >> 2) * STRIDE + LSB)[t & 3] = (u32x4){0, 0, 0, 0};
   // this lane's 16 profile bytes (a piece sits at the same offset of its band every pass)
   uint32_t pw[4];
   {
@@ -650,11 +655,7 @@ void k_subband_fast(SubArgs a) {
         reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
         reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
         if (pos == SEG - 1) {
-          // E[band][LSB] = T, then the zero tail E[band][LSB + 1 .. LSB + 31]
-          reinterpret_cast<u32x4*>(row + 16)[0] = (u32x4){excl + tot, 0, 0, 0};
-          reinterpret_cast<u32x4*>(row + 16)[1] = (u32x4){0, 0, 0, 0};
-          reinterpret_cast<u32x4*>(row + 16)[2] = (u32x4){0, 0, 0, 0};
-          reinterpret_cast<u32x4*>(row + 16)[3] = (u32x4){0, 0, 0, 0};
+          row[16] = (uint16_t)(excl + tot);  // E[band][LSB] = T (in the zeroed tail)
           bstat[3 * band + 0] = (int)(excl + tot);
           bstat[3 * band + 1] = X2;
           bstat[3 * band + 2] = XP;
@@ -697,30 +698,33 @@ void k_subband_fast(SubArgs a) {
     lo_k[k] = j < LSB ? j : LSB;
     hi_k[k] = j < nw ? j + wb : lo_k[k];
   }
-  // pass 1's layout (lane = band): band bi of the block, windows j = qtr + 4t, t < T; the
-  // steps run in chunks of 8 (skipped past T), and a window j >= nw of the last chunk reads
-  // E[j + wb] from the zero tail of its row (indices lsb + 1 .. lsb + 31), so its saturated
-  // difference is 0: no masks
+  // pass 1's layout (lane = band): band bi of the block; its quarter lane qtr takes the windows
+  // j = 8s + 2 qtr + p (step u = 2s + p), so at every step the four quarter lanes of a band
+  // read four distinct dwords and the 64 lanes 64 distinct banks (the row pitch is 4 x odd
+  // dwords); the steps run in chunks of 4 (skipped past the last window), and a window
+  // j >= nw of the last chunk reads E[j + wb] from the zero tail of its row (indices up to
+  // lsb + 22), so its saturated difference is 0: no masks
   const int bi = lane & 15, qtr = lane >> 4;
-  const int T = (nw + 3) >> 2;
-  constexpr int NCH = (LSB / 4 + 7) / 8;
+  const int U = 2 * ((nw + 7) >> 3);
+  constexpr int NCH = (LSB / 4 + 3) / 4;
   for (int blk = 0; blk < nsub; blk += SB_NB) {
     const int nb = nsub - blk < SB_NB ? nsub - blk : SB_NB;
     const uint16_t* rows = E + blk * STRIDE;  // bands past nsub are the zero rows
     // ---- pass 1: S = sum b, sum b^2 and the first maximum of each band -------------------
-    const uint16_t* plo = rows + bi * STRIDE + qtr;
+    const uint16_t* plo = rows + bi * STRIDE + 2 * qtr;
     const uint16_t* phi = plo + wb;
     int sv = 0, kl = 0;
     unsigned long long qv = 0;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      if (8 * ch < T) {  // wave-uniform
+      if (4 * ch < U) {  // wave-uniform
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int t = 8 * ch + u;
-          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[4 * t], (uint32_t)plo[4 * t]);
-          // the lane's own key: ties go to the smaller t (the smaller j of this lane)
-          const int kk = (int)((b << 6) | (uint32_t)(63 - t));
+        for (int v = 0; v < 4; ++v) {
+          const int u = 4 * ch + v;
+          const int o = 8 * (u >> 1) + (u & 1);
+          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
+          // the lane's own key: ties go to the smaller step (the smaller j of this lane)
+          const int kk = (int)((b << 6) | (uint32_t)(63 - u));
           kl = kk > kl ? kk : kl;
           sv += (int)b;
           // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
@@ -731,7 +735,8 @@ void k_subband_fast(SubArgs a) {
     }
     // the lane's best window as the band-wide key (b << 10) | (1023 - j), then the band's four
     // quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums and a maximum
-    int key = ((kl >> 6) << 10) | (1023 - (qtr + 4 * (63 - (kl & 63))));
+    const int ub = 63 - (kl & 63);
+    int key = ((kl >> 6) << 10) | (1023 - (8 * (ub >> 1) + 2 * qtr + (ub & 1)));
     sv += __shfl_xor(sv, 16);
     qv += xor_u64<16>(qv);
     key = max(key, __shfl_xor(key, 16));

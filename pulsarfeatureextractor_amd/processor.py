@@ -524,6 +524,7 @@ class RunMetrics:
         self.start_offset = int(start_offset)
         self.t0 = time.perf_counter()
         self.parse_s = 0.0
+        self.parse_span = None  # (first parse start, last parse end), seconds after t0
         self.score_s = 0.0
         self.stage = {}  # finer host timers of the GPU stage (pack, gpu), summed over slots
         self.batches = 0
@@ -541,7 +542,10 @@ class RunMetrics:
             try:
                 return fn(paths)
             finally:
-                self.parse_s += time.perf_counter() - t
+                e = time.perf_counter()
+                self.parse_s += e - t
+                first = self.parse_span[0] if self.parse_span else t - self.t0
+                self.parse_span = (first, e - self.t0)
         return wrapped
 
     def timed_score(self, fn):
@@ -570,6 +574,11 @@ class RunMetrics:
                 "batches": self.batches, "wall_s": round(wall, 6),
                 "candidates_per_s": round(processed / wall, 3) if wall > 0 else None,
                 "parse_s": round(self.parse_s, 6), "score_s": round(self.score_s, 6),
+                # where the parser was not busy: before its first batch, between batches
+                # (waiting for the pipeline), after its last
+                **({"parse_head_s": round(self.parse_span[0], 6),
+                    "parse_idle_s": round(self.parse_span[1] - self.parse_span[0] - self.parse_s, 6),
+                    "parse_tail_s": round(wall - self.parse_span[1], 6)} if self.parse_span else {}),
                 **{k + "_s": round(v, 6) for k, v in sorted(self.stage.items())}}
 
 
