@@ -122,6 +122,9 @@ int pfe_synchronize(pfe_handle* h);
  *   PFE_OPT_PFD_SPLIT    PFD preprocessing: 1 = the folds' part sums streamed by their own kernel
  *                        on a side stream while the sweep kernel works on the previous chunk,
  *                        0 = one fused kernel (default; same bits)
+ *   PFE_OPT_LYON8_DM_SPLIT  1 (default): the last numpy chunk of a DataBlock row with <= 32
+ *                        leaves is summed by 2, 4 or 8 lanes per leaf, each taking some of the
+ *                        leaf's 8 chains; 0: one lane per leaf (same bits)
  * Returns PFE_EINVAL for an unknown option or an out-of-range value.
  * --------------------------------------------------------------------------------------- */
 #define PFE_OPT_SOLVER 1
@@ -133,6 +136,7 @@ int pfe_synchronize(pfe_handle* h);
 #define PFE_OPT_PFD_WAVES 7
 #define PFE_OPT_LYON8_DM 8
 #define PFE_OPT_PFD_SPLIT 9
+#define PFE_OPT_LYON8_DM_SPLIT 10
 #define PFE_SOLVER_POOLED 0
 #define PFE_SOLVER_BATCHED 1
 #define PFE_SOLVER_WAVE 2

@@ -285,6 +285,10 @@ int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
       if (v != 0 && v != 1) break;
       o.pfd_split = (int)v;
       return PFE_OK;
+    case PFE_OPT_LYON8_DM_SPLIT:
+      if (v != 0 && v != 1) break;
+      o.lyon8_dm_split = (int)v;
+      return PFE_OK;
     default:
       return set_err(h, PFE_EINVAL, "pfe_set_option: unknown option %d", option);
   }
@@ -305,6 +309,7 @@ int pfe_get_option(const pfe_handle* h, int32_t option, int64_t* v) {
     case PFE_OPT_PFD_WAVES: *v = o.pfd_waves; return PFE_OK;
     case PFE_OPT_LYON8_DM: *v = o.lyon8_dm; return PFE_OK;
     case PFE_OPT_PFD_SPLIT: *v = o.pfd_split; return PFE_OK;
+    case PFE_OPT_LYON8_DM_SPLIT: *v = o.lyon8_dm_split; return PFE_OK;
     default: return PFE_EINVAL;
   }
 }

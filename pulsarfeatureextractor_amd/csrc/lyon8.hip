@@ -798,21 +798,29 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 //     so the leaf sum is numpy's times 2^-102 exactly (the caller scales it back).
 // FPM adds scipy's d^3 = d^2 * d and d^4 = (d^2)^2 as fused running sums (scaled 2^-153 and
 // 2^-204), in any order.  Words past the leaf (k >= nw) are read inside the image, not added.
-template <bool FPM>
-__device__ __forceinline__ double dm_leaf(const uint8_t* lb, double nm, double sc,
+//
+// NC < 8 (round 5, the last chunk of a row whose <= 32 leaves would leave lanes idle): the
+// lane takes only the NC chains c0 .. c0 + NC - 1 of its leaf (G = 8 / NC lanes per leaf) and
+// returns their part of the leaf's tree -- (r0+r1)+(r2+r3) of its four chains, r0+r1 of two,
+// r0 of one -- so the first log2(G) steps of the wave butterfly that follows complete each
+// leaf's ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) with numpy's bits and the remaining steps are the
+// tree over the leaves, as before: the pass reads and squares 128/G bytes per lane.
+template <bool FPM, int NC = 8>
+__device__ __forceinline__ double dm_leaf(const uint8_t* lb, int c0, double nm, double sc,
                                           const uint32_t (&z)[8], int nw, double& a3, double& a4) {
+  static_assert(NC == 1 || NC == 2 || NC == 4 || NC == 8, "chains per lane");
   typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
-  lds_u8* vb = (lds_u8*)lb;
-  double r[8];
+  lds_u8* vb = (lds_u8*)(lb + c0);
+  double r[NC];
   double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    uint32_t x[8];
+    uint32_t x[NC];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = vb[8 * k + j];
+    for (int j = 0; j < NC; ++j) x[j] = vb[8 * k + j];
     if (k < 8 || k < nw) {  // leaves hold >= 8 words: the first eight need no lane test
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < NC; ++j) {
         const double X = __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]);
         const double d = __builtin_fma(sc, X, nm);
         const double sq = d * d;
@@ -825,13 +833,16 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, double nm, double s
     }
     // pin word k's arithmetic before word k+1's reads (empty asm ordered with the volatile
     // reads; without it every read of the leaf is hoisted, one VGPR each)
-    asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
-                 "+v"(r[6]), "+v"(r[7]));
+#pragma unroll
+    for (int j = 0; j < NC; ++j) asm volatile("" : "+v"(r[j]));
     if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
   }
   a3 = c3[0] + c3[1];
   a4 = c4[0] + c4[1];
-  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  if constexpr (NC == 8) return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  if constexpr (NC == 4) return (r[0] + r[1]) + (r[2] + r[3]);
+  if constexpr (NC == 2) return r[0] + r[1];
+  return r[0];
 }
 
 // write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image.  Full
@@ -881,11 +892,14 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
 #ifndef PFE_DM_WPE_LONG
 #define PFE_DM_WPE_LONG 3  // waves per SIMD of the 3- and 4-chunk forms (nDM > 128)
 #endif
-template <int NCH, bool FPM>
+// G: lanes per leaf of the last chunk (1; or 2 / 4 / 8 when it has <= 32 / 16 / 8 leaves,
+// see dm_leaf)
+template <int NCH, bool FPM, int G = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 4 : PFE_DM_WPE_LONG, NCH <= 2 ? 4 : PFE_DM_WPE_LONG)))
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per leaf");
   constexpr int NPMAX = 8 * NCH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
   __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
@@ -917,7 +931,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
   // this lane's leaf of the last chunk (-1: none) and its 8-byte words
   const int leaf_last = sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
-                               : (lane < sh.leaves_last ? lane : -1);
+                               : (lane / G < sh.leaves_last ? lane / G : -1);
   const int nw_last = leaf_last >= 0 ? (sh.start[leaf_last + 1] - sh.start[leaf_last]) >> 3 : 16;
   // dm_leaf's constants: eight zeros held in registers (the high halves of the byte pairs)
   // and 2^1023 in an SGPR pair (a VOP3 operand; as a literal it would cost a move per byte)
@@ -988,7 +1002,11 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         if (ch > 0) dm_stage<NCH>(img, q, ch, lane, full_base, stab);
         wave_lds_sync();
         double l3, l4;
-        double leaf = dm_leaf<FPM>(img + lane * DM_S, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
+        double leaf;
+        if (G > 1 && ch == NCH - 1)  // the last chunk's leaf lane / G, chains of this lane
+          leaf = dm_leaf<FPM, 8 / G>(img + (lane / G) * DM_S, (8 / G) * (lane % G), nm, sc, z, nw_last, l3, l4);
+        else
+          leaf = dm_leaf<FPM>(img + lane * DM_S, 0, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
           const bool in = leaf_last >= 0;
           leaf = in ? leaf : 0.0;
@@ -1232,10 +1250,10 @@ static int resident_blocks() {
 #ifndef PFE_DM_FPM_MAXCH
 #define PFE_DM_FPM_MAXCH 4
 #endif
-template <int NCH, bool FPM>
+template <int NCH, bool FPM, int G = 1>
 static void launch_dm_kernel(const uint8_t* prof, int64_t ps, const uint8_t* dm, int64_t ds,
                              int64_t n, double* out, const DmShape& sh, hipStream_t st, int cap) {
-  constexpr auto K = lyon8_u8_dm<NCH, FPM>;
+  constexpr auto K = lyon8_u8_dm<NCH, FPM, G>;
   int64_t blocks = resident_blocks<K>();
   const int64_t need = (n + 3) / 4;  // at least one row per wave
   if (blocks > need) blocks = need;
@@ -1258,15 +1276,27 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     // §3.1c), skew / kurt from fp64 d^3 / d^4 sums (the faster form at every length
     // measured), from the exact power sums with option 2
     const int cap = o.lyon8_blocks;
+    // lanes per leaf of the last chunk: a last chunk of <= 32 leaves is split by chains
+    // (PFE_OPT_LYON8_DM_SPLIT = 0 keeps one lane per leaf)
+    const int G = (dsh.tri || !o.lyon8_dm_split) ? 1
+                  : dsh.leaves_last <= 8 ? 8 : dsh.leaves_last <= 16 ? 4 : dsh.leaves_last <= 32 ? 2 : 1;
     if (o.lyon8_dm == 0 && dnch <= PFE_DM_FPM_MAXCH) {
+#define PFE_DMK(C)                                                                   \
+  switch (G) {                                                                       \
+    case 8: launch_dm_kernel<C, true, 8>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    case 4: launch_dm_kernel<C, true, 4>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    case 2: launch_dm_kernel<C, true, 2>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    default: launch_dm_kernel<C, true, 1>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+  }
       switch (dnch) {
-        case 1: launch_dm_kernel<1, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-        case 2: launch_dm_kernel<2, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+        case 1: PFE_DMK(1) break;
+        case 2: PFE_DMK(2) break;
 #if PFE_DM_FPM_MAXCH > 2
-        case 3: launch_dm_kernel<3, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
-        default: launch_dm_kernel<4, true>(prof, ps, dm, ds, n, out, dsh, st, cap); break;
+        case 3: PFE_DMK(3) break;
+        default: PFE_DMK(4) break;
 #endif
       }
+#undef PFE_DMK
     } else {
       switch (dnch) {
         case 1: launch_dm_kernel<1, false>(prof, ps, dm, ds, n, out, dsh, st, cap); break;

@@ -18,6 +18,7 @@ struct Options {
   int pfd_waves = 4;               // waves per fold of the PFD dmprof kernel (4 or 1)
   int lyon8_dm = 0;                // DataBlock DM rows (pfe.h PFE_OPT_LYON8_DM, 0..2)
   int pfd_split = 0;               // PFD dmprof: 1 part sums by k_pfd_parts beside the sweep, 0 fused
+  int lyon8_dm_split = 1;          // DataBlock rows: chain-split last chunks of <= 32 leaves
 };
 
 }  // namespace pfe
