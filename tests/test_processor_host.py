@@ -355,3 +355,34 @@ def test_stream_over_a_path_feed_still_being_walked():
         len(PathFeed(broken()))
     assert len(PathFeed(iter([]))) == 0
     _stream(PathFeed(iter([])), None, None, None)  # nothing listed: no batch, no call
+
+
+def test_discover_streams_large_directories_in_os_walk_order(tmp_path):
+    """The streamed walk (listing chunks of 2048 entries) gives exactly os.walk + fnmatch's
+    paths and order: a 5000-entry directory with non-matching names mixed in, nested
+    subdirectories, a symlinked directory (listed by os.walk, not entered) and a symlinked
+    file (matched as a file)."""
+    import fnmatch
+
+    big = tmp_path / "big"
+    (big / "sub" / "deeper").mkdir(parents=True)
+    for i in range(5000):
+        (big / (f"c{i}.phcx.gz" if i % 3 else f"c{i}.txt")).write_text("")
+    for p in ("sub/a.phcx.gz", "sub/deeper/b.phcx.gz", "sub/c.pfd"):
+        (big / p).write_text("")
+    os.symlink(big / "sub", big / "linked_dir")
+    os.symlink(big / "c1.phcx.gz", big / "zz_link.phcx.gz")
+
+    def ref(directory, regexes):
+        out = []
+        for ft in regexes:
+            for root, _s, fns in os.walk(directory):
+                out.extend(os.path.join(root, fn) for fn in fnmatch.filter(fns, ft))
+        return out
+
+    for d in (str(big), str(big) + "/"):
+        for pats in ([processor.PHCX_RE], [processor.PHCX_RE] + list(processor.PFD_RES)):
+            got = processor.discover(d, pats)
+            assert got == ref(d, pats) and len(got) > 3000
+    chunks = list(processor.iter_discover(str(big), [processor.PHCX_RE]))
+    assert len(chunks) >= 3  # streamed while the big directory is listed
