@@ -460,7 +460,8 @@ def run_lyon8(ctx, args, n, lp):
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     # HBM bytes per launch: the round-4 PMC passes of this command at the current defaults
     # (tools/gpu_steps.sh trace_l8 pmc_l8 -> tools/summarize_prof.py); round 2's if absent
-    traffic = (load_traffic(f"r04_lyon8_u8_{lp}x{args.ld}_n{n}.json")
+    traffic = (load_traffic(f"r05_lyon8_u8_{lp}x{args.ld}_n{n}.json")
+               or load_traffic(f"r04_lyon8_u8_{lp}x{args.ld}_n{n}.json")
                or load_traffic(f"lyon8_u8_{lp}x{args.ld}_n{n}_pmc.json"))
     return {
         "metric": "candidates/sec (8-feature path, 128-bin)",
