@@ -845,6 +845,78 @@ __device__ __forceinline__ double dm_leaf(const uint8_t* lb, int c0, double nm, 
   return r[0];
 }
 
+// The tri form's last chunk split by chains (G == 3 of lyon8_u8_dm): block b's quad takes
+//   q0: the 128-byte leaf's chains 0-3, q3: its chains 4-7 (16 words of 4 bytes each),
+//   q1: the 64-byte leaf, chains 0-3 over its 8 words then chains 4-7 (restart at step 8),
+//   q2: the 72-byte leaf, chains 0-3 over its 9 words then chains 4-7 (restart at step 9),
+// one loop of 18 steps of 4 bytes (q2's 72 bytes; the others' steps past 16 add nothing)
+// instead of one lane reading all 128 bytes of the big leaf.  Every chain still adds its
+// bytes in order; q0 returns A = (r0+r1)+(r2+r3), q3 B = (r4+r5)+(r6+r7) (the big leaf is
+// A + B), q1 / q2 their whole leaves.  Image slots as the tri stab has them: the big leaf at
+// 4b (read by q0 and q3), the others at 4b + 1, 4b + 2.
+template <bool FPM>
+__device__ __forceinline__ double dm_leaf_tri(const uint8_t* img, int lane, double nm, double sc,
+                                              const uint32_t (&z)[8], double& a3, double& a4) {
+  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
+  const int q = lane & 3;
+  const uint8_t* leaf = img + (q == 3 ? lane - 3 : lane) * DM_S;
+  // step k reads 4 bytes at: b1 + 8k (k < 8), base8 (k = 8), base9 + 8(k - 9) (k >= 9).  The
+  // chains 0-3 stream (b1 + 8k) runs until the lane's restart R, then chains 4-7 of word
+  // k - R are at leaf + 4 + 8(k - R) (R = 8 for q1, 9 for q2; none for q0 / q3)
+  const uint8_t* b1 = leaf + (q == 3 ? 4 : 0);
+  const uint8_t* base8 = q == 1 ? leaf + 4 : b1 + 64;
+  const uint8_t* base9 = q == 1 ? leaf + 12 : q == 2 ? leaf + 4 : b1 + 72;
+  double r[4], sv[4] = {0.0, 0.0, 0.0, 0.0};
+  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 18; ++k) {
+    lds_u8* vb = (lds_u8*)(k < 8 ? b1 + 8 * k : k == 8 ? base8 : base9 + 8 * (k - 9));
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = vb[i];
+    if (k == 8 || k == 9) {  // the 64 / 72-byte leaf's restart: chains 0-3 done
+      const bool rs = q == k - 7;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sv[i] = rs ? r[i] : sv[i];
+        r[i] = rs ? 0.0 : r[i];
+      }
+    }
+    const bool valid = k < 16 || q == 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double X = __builtin_bit_cast(double, ((uint64_t)z[i] << 32) | x[i]);
+      const double d = __builtin_fma(sc, X, nm);
+      double sq = d * d;
+      if (k >= 16) sq = valid ? sq : 0.0;  // +0.0 leaves a non-negative sum's bits alone
+      r[i] = k == 0 ? sq : r[i] + sq;
+      if constexpr (FPM) {
+        c3[i & 1] = __builtin_fma(sq, d, c3[i & 1]);
+        c4[i & 1] = __builtin_fma(sq, sq, c4[i & 1]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(r[i]), "+v"(sv[i]));
+    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
+  }
+  a3 = c3[0] + c3[1];
+  a4 = c4[0] + c4[1];
+  const double tr = (r[0] + r[1]) + (r[2] + r[3]);
+  const double ts = (sv[0] + sv[1]) + (sv[2] + sv[3]);
+  return (q == 1 || q == 2) ? ts + tr : tr;
+}
+
+// numpy's sum of the tri form's 48 leaves from dm_leaf_tri's parts: the big leaf as q0 + q3
+// and the pair as q1 + q2 (quad_perm [3,2,1,0]), the block as big + pair -- the bits of
+// wave_sum_tri_f64's l0 + (l1 + l2) -- then the 16 blocks pairwise
+__device__ __forceinline__ double wave_sum_tri_split_f64(double v) {
+  v += dpp_f64<0x1B>(v);
+  v = dpp_f64<0x00>(v) + dpp_f64<0x55>(v);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f64<DPP_ROW_MIRROR>(v);
+  return row_total_f64(v);
+}
+
 // write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image.  Full
 // chunks: leaf lane/8 + 8j at offset 16 (lane % 8).  The last chunk: each 8-byte half at the
 // address of the block's table stab (0xFFFF: past the chunk).
@@ -899,7 +971,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
-  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per leaf");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 3, "lanes per leaf (3: the tri form split)");
   constexpr int NPMAX = 8 * NCH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
   __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
@@ -930,7 +1002,8 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
   // this lane's leaf of the last chunk (-1: none) and its 8-byte words
-  const int leaf_last = sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
+  const int leaf_last = G == 3 ? 0  // every lane of the split tri form holds a part
+                      : sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
                                : (lane / G < sh.leaves_last ? lane / G : -1);
   const int nw_last = leaf_last >= 0 ? (sh.start[leaf_last + 1] - sh.start[leaf_last]) >> 3 : 16;
   // dm_leaf's constants: eight zeros held in registers (the high halves of the byte pairs)
@@ -1003,8 +1076,10 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         wave_lds_sync();
         double l3, l4;
         double leaf;
-        if (G > 1 && ch == NCH - 1)  // the last chunk's leaf lane / G, chains of this lane
-          leaf = dm_leaf<FPM, 8 / G>(img + (lane / G) * DM_S, (8 / G) * (lane % G), nm, sc, z, nw_last, l3, l4);
+        if (G == 3 && ch == NCH - 1)  // the tri form, its big leaf split by chains
+          leaf = dm_leaf_tri<FPM>(img, lane, nm, sc, z, l3, l4);
+        else if (G > 1 && G != 3 && ch == NCH - 1)  // the last chunk's leaf lane / G, chains of this lane
+          leaf = dm_leaf<FPM, (G == 3 ? 1 : 8 / G)>(img + (lane / G) * DM_S, (8 / G) * (lane % G), nm, sc, z, nw_last, l3, l4);
         else
           leaf = dm_leaf<FPM>(img + lane * DM_S, 0, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
@@ -1016,7 +1091,8 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         a3 += l3;
         a4 += l4;
         // numpy's tree over the lane-ordered leaves (the tri form: two depths)
-        const double cs = (ch == NCH - 1 && sh.tri) ? wave_sum_tri_f64(leaf) : wave_sum_f64(leaf);
+        const double cs = (ch == NCH - 1 && G == 3) ? wave_sum_tri_split_f64(leaf)
+                          : (ch == NCH - 1 && sh.tri) ? wave_sum_tri_f64(leaf) : wave_sum_f64(leaf);
         ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order (all scaled by 2^-102)
         wave_lds_sync();
       }
@@ -1278,7 +1354,8 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     const int cap = o.lyon8_blocks;
     // lanes per leaf of the last chunk: a last chunk of <= 32 leaves is split by chains
     // (PFE_OPT_LYON8_DM_SPLIT = 0 keeps one lane per leaf)
-    const int G = (dsh.tri || !o.lyon8_dm_split) ? 1
+    const int G = !o.lyon8_dm_split ? 1
+                  : dsh.tri ? 3  // the tri form's big leaf split by chains
                   : dsh.leaves_last <= 8 ? 8 : dsh.leaves_last <= 16 ? 4 : dsh.leaves_last <= 32 ? 2 : 1;
     if (o.lyon8_dm == 0 && dnch <= PFE_DM_FPM_MAXCH) {
 #define PFE_DMK(C)                                                                   \
@@ -1286,6 +1363,7 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     case 8: launch_dm_kernel<C, true, 8>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 4: launch_dm_kernel<C, true, 4>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 2: launch_dm_kernel<C, true, 2>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    case 3: launch_dm_kernel<C, true, 3>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     default: launch_dm_kernel<C, true, 1>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
   }
       switch (dnch) {
