@@ -110,7 +110,7 @@ int pfe_synchronize(pfe_handle* h);
  *   PFE_OPT_HANDOVER     0: re-evaluate the residuals after an accepted LM step instead of
  *                        handing the trial's residuals over (default 1)
  *   PFE_OPT_GSLOTS       fit slots per pooled wave, 1..32 (0 = sized from n; default 0)
- *   PFE_OPT_LYON8_BLOCKS grid cap of the Lyon-8 stream kernel (default 16384)
+ *   PFE_OPT_LYON8_BLOCKS grid cap of the Lyon-8 kernels (default 131072)
  *   PFE_OPT_LYON8_BURST  candidate groups per wave step of the Lyon-8 kernel: 1, 2 or 4
  *                        (default 2)
  *   PFE_OPT_PFD_WAVES    waves per fold of the PFD preprocessing kernel: 4 (default) or 1

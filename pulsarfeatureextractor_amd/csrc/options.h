@@ -13,7 +13,7 @@ struct Options {
   int serial = 0;                  // 1: score groups in order on the handle's stream
   int handover = 1;                // 0: re-evaluate the function after accepted LM steps
   int gslots = 0;                  // fit slots per pooled wave (0: sized from n and the CUs)
-  int lyon8_blocks = 16384;        // grid cap of the Lyon-8 stream kernel
+  int lyon8_blocks = 131072;       // grid cap of the Lyon-8 stream kernel
   int lyon8_burst = 2;             // candidate groups per wave step of the Lyon-8 kernel
   int pfd_waves = 4;               // waves per fold of the PFD dmprof kernel (4 or 1)
   int lyon8_dm = 0;                // DataBlock DM rows (pfe.h PFE_OPT_LYON8_DM, 0..2)

@@ -269,6 +269,11 @@ int main(int argc, char** argv) {
     run("split: read 256 B only g16384", [&] { hipLaunchKernelGGL((k_rows_half<1, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
     run("split: write 64 B only g16384", [&] { hipLaunchKernelGGL((k_rows_half<2, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
     run("split: read+write g16384", [&] { hipLaunchKernelGGL((k_rowsU<1, 1, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write, plain stores", [&] { hipLaunchKernelGGL((k_rowsU<1, 0, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write, plain loads", [&] { hipLaunchKernelGGL((k_rowsU<0, 1, 2>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write, U4", [&] { hipLaunchKernelGGL((k_rowsU<1, 1, 4>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write g8192", [&] { hipLaunchKernelGGL((k_rowsU<1, 1, 2>), dim3(8192), dim3(256), 0, 0, a, b, o, n); });
+    run("split: read+write g32768", [&] { hipLaunchKernelGGL((k_rowsU<1, 1, 2>), dim3(32768), dim3(256), 0, 0, a, b, o, n); });
     run("copy (3.2GB moved) g16384", [&] { hipLaunchKernelGGL(k_copy, dim3(16384), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n * 10); });
   }
   for (int rep = 0; rep < 2; ++rep)
