@@ -432,13 +432,14 @@ __global__ __launch_bounds__(64 * WPB) void k_subband2(SubArgs a) {
 //     the order -- numpy's d = sum (x-mu)(p-pm) equals (L XP - T P)/L exactly, with
 //     XP = sum x p, T = sum x, P = sum p (likewise sum (x-mu)^2 and the profile's): three
 //     v_dot4 sums per 16-byte piece, taken in the same pass that builds the prefix sums;
-//   * s20 / s21: boxcar sums and their S, sum b^2 in integers; per-band reductions are
-//     reduce-scatters (16 bands over the 16 lanes of a row: 15 exchanges instead of 16 x 6);
-//     the s21 identity of k_subband2 with W_j = sum_i r_i b_ij accumulated by fma;
-//   * no masks in the window loop: the prefix rows are padded with zero rows to a multiple of
-//     16 bands, and a window past the last one reads the same prefix twice, so its boxcar sum
-//     is 0 by construction and its key (0 << 10 | 1023 - j) loses to every real window
-//     (those have smaller j).
+//   * s20 / s21 in two passes over each block of 16 bands (round 5): pass 1 puts a band in
+//     each lane (16 bands x 4 quarter lanes), so S = sum b, sum b^2 and the first maximum of
+//     a band need two cross-lane steps; pass 2 (lane = window) forms the s21 identity of
+//     k_subband2, W_j = sum_i r_i b_ij in band order, by fma;
+//   * no masks in either pass: the prefix rows are padded with zero rows to a multiple of 16
+//     bands and carry a zero tail; a pass-1 window past the last one reads the tail (its
+//     saturated difference is 0), a pass-2 window reads the same prefix twice, so its boxcar
+//     sum is 0 and its key (0 << 10 | 1023 - j) loses to every real window (smaller j).
 __host__ __device__ constexpr int sb_pad16(int nsub) { return (nsub + 15) & ~15; }
 // the fast kernel's u16 row pitch: lsb + 1 prefixes and a zero tail to lsb + 31 (read by the
 // band-per-lane pass past the last window), 16-B aligned rows, and a pitch of 4 x odd dwords so
@@ -487,65 +488,8 @@ __device__ __forceinline__ unsigned long long xor_u64(unsigned long long v) {
   const int hi = xor_i32<M>((int)(uint32_t)(v >> 32));
   return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
 }
-template <int M>
-__device__ __forceinline__ int xor_v(int v) { return xor_i32<M>(v); }
-template <int M>
-__device__ __forceinline__ unsigned long long xor_v(unsigned long long v) { return xor_u64<M>(v); }
-
-// one reduce-scatter step: lanes with bit M keep the upper H entries, the others the lower
-template <int M, int H, typename T, typename Op>
-__device__ __forceinline__ void rs_step(T (&v)[16], int lane, Op op) {
-  const bool hi = (lane & M) != 0;
-#pragma unroll
-  for (int t = 0; t < H; ++t) {
-    const T keep = hi ? v[t + H] : v[t];
-    const T send = hi ? v[t] : v[t + H];
-    v[t] = op(keep, xor_v<M>(send));
-  }
-}
-// 16 per-lane values -> v[0] of lane l = the wave total of entry bitrev4(l & 15)
-template <typename T, typename Op>
-__device__ __forceinline__ void reduce_scatter16(T (&v)[16], int lane, Op op) {
-  rs_step<1, 8>(v, lane, op);
-  rs_step<2, 4>(v, lane, op);
-  rs_step<4, 2>(v, lane, op);
-  rs_step<8, 1>(v, lane, op);
-  v[0] = op(v[0], xor_v<16>(v[0]));
-  v[0] = op(v[0], xor_v<32>(v[0]));
-}
-// The same reduce-scatter with every in-row exchange on DPP (no ds_bpermute): the partners
-// are i^15 (row_mirror), i^7 (row_half_mirror), i^3 and i^1 (quad_perm), each differing from
-// the lane in the bit its step splits on and agreeing in the bits earlier steps split on, so
-// after the four steps each lane of a row has summed all 16 lanes; lane l holds entry l & 15
-template <int CTRL>
-__device__ __forceinline__ int dpp_x(int v) { return dpp_i32<CTRL>(v); }
-template <int CTRL>
-__device__ __forceinline__ unsigned long long dpp_x(unsigned long long v) { return dpp_u64<CTRL>(v); }
-template <int M, int H, int CTRL, typename T, typename Op>
-__device__ __forceinline__ void rs_step_dpp(T (&v)[16], int lane, Op op) {
-  const bool hi = (lane & M) != 0;
-#pragma unroll
-  for (int t = 0; t < H; ++t) {
-    const T keep = hi ? v[t + H] : v[t];
-    const T send = hi ? v[t] : v[t + H];
-    v[t] = op(keep, dpp_x<CTRL>(send));
-  }
-}
-template <typename T, typename Op>
-__device__ __forceinline__ void reduce_scatter16_dpp(T (&v)[16], int lane, Op op) {
-  rs_step_dpp<8, 8, DPP_ROW_MIRROR>(v, lane, op);
-  rs_step_dpp<4, 4, DPP_ROW_HALF_MIRROR>(v, lane, op);
-  rs_step_dpp<2, 2, 0x1B>(v, lane, op);  // quad_perm [3,2,1,0]
-  rs_step_dpp<1, 1, DPP_QUAD_XOR1>(v, lane, op);
-  v[0] = op(v[0], xor_v<16>(v[0]));
-  v[0] = op(v[0], xor_v<32>(v[0]));
-}
-__device__ __forceinline__ int bitrev4(int l) {
-  return ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
-}
-
 #ifndef PFE_SUBBAND_WPE
-#define PFE_SUBBAND_WPE 3  // 3 waves per SIMD at 256 bins (168 VGPRs)
+#define PFE_SUBBAND_WPE 3  // register cap (168 VGPRs); the two-pass kernel uses 64-74
 #endif
 template <int LSB, int WPB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PFE_SUBBAND_WPE)))
