@@ -79,7 +79,7 @@ OPTIONS = {
     "pfd_waves": 7,
     "lyon8_dm": 8,      # DataBlock kernels: 0 default, 1 round 3, 2 exact power sums (pfe.h)
     "pfd_split": 9,     # 0 fused kernel (default), 1 part sums streamed beside the sweep
-    "lyon8_dm_split": 10,  # 1 (default): last DataBlock chunks of <= 32 leaves split by chains
+    "lyon8_dm_split": 10,  # 1 (default) chain splits + paired one-chunk rows, 2 splits only, 0 off
 }
 SOLVERS = {"pooled": 0, "batched": 1, "wave": 2}
 

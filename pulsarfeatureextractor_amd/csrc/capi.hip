@@ -286,7 +286,7 @@ int pfe_set_option(pfe_handle* h, int32_t option, int64_t v) {
       o.pfd_split = (int)v;
       return PFE_OK;
     case PFE_OPT_LYON8_DM_SPLIT:
-      if (v != 0 && v != 1) break;
+      if (v < 0 || v > 2) break;
       o.lyon8_dm_split = (int)v;
       return PFE_OK;
     default:

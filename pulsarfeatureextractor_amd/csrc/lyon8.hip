@@ -917,6 +917,24 @@ __device__ __forceinline__ double wave_sum_tri_split_f64(double v) {
   return row_total_f64(v);
 }
 
+// Sums over each 32-lane half of the wave (two rows per wave, G == 16 of lyon8_u8_dm): the
+// in-row DPP steps of wave_sum_* and one exchange with lane ^ 16 -- for 32 leaves numpy's
+// (tree of 0..15) + (tree of 16..31), for fewer the rows past them add +0.0
+__device__ __forceinline__ uint32_t half_sum_u32(uint32_t v) {
+  v += (uint32_t)dpp_i32<DPP_QUAD_XOR1>((int)v);
+  v += (uint32_t)dpp_i32<DPP_QUAD_XOR2>((int)v);
+  v += (uint32_t)dpp_i32<DPP_ROW_HALF_MIRROR>((int)v);
+  v += (uint32_t)dpp_i32<DPP_ROW_MIRROR>((int)v);
+  return v + (uint32_t)__shfl_xor((int)v, 16);
+}
+__device__ __forceinline__ double half_sum_f64(double v) {
+  v += dpp_f64<DPP_QUAD_XOR1>(v);
+  v += dpp_f64<DPP_QUAD_XOR2>(v);
+  v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f64<DPP_ROW_MIRROR>(v);
+  return v + __shfl_xor(v, 16);
+}
+
 // write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image.  Full
 // chunks: leaf lane/8 + 8j at offset 16 (lane % 8).  The last chunk: each 8-byte half at the
 // address of the block's table stab (0xFFFF: past the chunk).
@@ -971,22 +989,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
-  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 3, "lanes per leaf (3: the tri form split)");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 3 || G == 16,
+                "lanes per leaf (3: the tri form split; 16: two one-chunk rows per wave)");
+  // G == 16: one-chunk rows of <= 32 leaves two at a time, row c in lanes 0-31 and row c + 1
+  // in lanes 32-63 (one leaf per lane, every per-row step shared by two rows)
+  constexpr bool PAIR = G == 16;
+  static_assert(!PAIR || (NCH == 1 && FPM), "pairs: one-chunk rows, fp64 moments");
   constexpr int NPMAX = 8 * NCH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
   __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
   const int lane = threadIdx.x & 63;
   uint8_t* img = lds[threadIdx.x >> 6];
   // the block's staging table (row-invariant): half h of lane l's piece j holds chunk bytes
-  // o = 16 l + 1024 j + 8 h, i.e. bytes o - start(L) of leaf L
+  // o = 16 l + 1024 j + 8 h, i.e. bytes o - start(L) of leaf L (pairs: o = 16 (l % 32) +
+  // 512 j + 8 h of the half's row, its leaf L at slot 32 (l / 32) + L)
   for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {
     const int jh = e >> 6, l = e & 63;
-    const int o = 16 * l + 1024 * (jh >> 1) + 8 * (jh & 1);
+    const int o = PAIR ? 16 * (l & 31) + 512 * (jh >> 1) + 8 * (jh & 1)
+                       : 16 * l + 1024 * (jh >> 1) + 8 * (jh & 1);
     uint16_t a = 0xFFFFu;
     if (o < sh.len_last) {
       int L = 0;
       while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
-      a = (uint16_t)(dm_leaf_lane(sh, L) * DM_S + (o - sh.start[L]));
+      a = (uint16_t)(((PAIR ? 32 * (l >> 5) : 0) + dm_leaf_lane(sh, L)) * DM_S + (o - sh.start[L]));
     }
     stab[e] = a;
   }
@@ -1003,6 +1028,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
   // this lane's leaf of the last chunk (-1: none) and its 8-byte words
   const int leaf_last = G == 3 ? 0  // every lane of the split tri form holds a part
+                      : PAIR ? ((lane & 31) < sh.leaves_last ? (lane & 31) : -1)
                       : sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
                                : (lane / G < sh.leaves_last ? lane / G : -1);
   const int nw_last = leaf_last >= 0 ? (sh.start[leaf_last + 1] - sh.start[leaf_last]) >> 3 : 16;
@@ -1020,16 +1046,28 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
     const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
     uint32_t kS1 = 0, kS2 = 0, kT3l = 0, kT3h = 0, kT4l = 0, kT4h = 0;
     double kssq = 0.0;
-    for (int i = 0; i < cnt; ++i) {
+    for (int i = 0; i < cnt; i += PAIR ? 2 : 1) {
       const int64_t c = base + i;
-      // ---- loads: piece p = lane + 64 k (16 B) through a buffer descriptor of the row's
-      // ld bytes, so pieces past the row read as zero bytes (corrected below)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint8_t*>(dm + c * ds), 0, sh.ld, 0x00020000);
+      const bool two = PAIR && i + 1 < cnt;  // pairs: is there a row c + 1 (lanes 32-63)?
       u32x4 q[NPMAX];
+      if constexpr (PAIR) {
+        // piece p = lane % 32 + 32 k of the half's row (a lone last row: both halves read it)
+        const uint8_t* rowp = dm + (c + (two ? (lane >> 5) : 0)) * ds;
 #pragma unroll
-      for (int k = 0; k < NPMAX; ++k)
-        q[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * k, 2));
+        for (int k = 0; k < NPMAX; ++k) {
+          const int p = (lane & 31) + 32 * k;
+          q[k] = 16 * p < sh.ld ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowp) + p)
+                                : (u32x4){0u, 0u, 0u, 0u};
+        }
+      } else {
+        // ---- loads: piece p = lane + 64 k (16 B) through a buffer descriptor of the row's
+        // ld bytes, so pieces past the row read as zero bytes (corrected below)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(dm + c * ds), 0, sh.ld, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < NPMAX; ++k)
+          q[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * k, 2));
+      }
       // ---- exact power sums of the DM row; a zero byte past the row adds y^3 = -2^21 and
       // y^4 = 2^28 (y = x - 128) and nothing to sum x, sum x^2
       Acc2 sd = {0, 0, 0, 0};
@@ -1050,13 +1088,24 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
       // ---- numpy's sum of squared deviations, chunk by chunk through the LDS image
       // (chunk 0 is staged before the mean is known, so its registers die early)
       dm_stage<NCH>(img, q, 0, lane, full_base, stab);
-      const uint32_t S1 = wave_sum_u32(sd.s1);
+      const uint32_t S1 = PAIR ? half_sum_u32(sd.s1) : wave_sum_u32(sd.s1);
       const double mean = (double)S1 / (double)sh.ld;
       const double nm = -__builtin_ldexp(mean, -51);  // exact
       // ---- the integer row totals (exact 32-bit halves) are reduced and parked in lane i
       // now, so their registers are free during the byte loop
+      // park row c's value in lane i (pairs: row c + 1's, from lane 32, in lane i + 1)
       const bool mine = lane == i;
-      kS1 = mine ? S1 : kS1;
+      const bool mine2 = two && lane == i + 1;
+      auto park_u32 = [&](uint32_t& k, uint32_t v) {
+        if constexpr (PAIR) {
+          const uint32_t va = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+          const uint32_t vb = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+          k = mine ? va : mine2 ? vb : k;
+        } else {
+          k = mine ? v : k;
+        }
+      };
+      park_u32(kS1, S1);
       if constexpr (!FPM) {
         const uint32_t S2 = wave_sum_u32(sd.s2);
         const uint32_t T3l = wave_sum_u32((uint32_t)sd.t3 & 0xFFFFu);
@@ -1078,8 +1127,13 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         double leaf;
         if (G == 3 && ch == NCH - 1)  // the tri form, its big leaf split by chains
           leaf = dm_leaf_tri<FPM>(img, lane, nm, sc, z, l3, l4);
-        else if (G > 1 && G != 3 && ch == NCH - 1)  // the last chunk's leaf lane / G, chains of this lane
-          leaf = dm_leaf<FPM, (G == 3 ? 1 : 8 / G)>(img + (lane / G) * DM_S, (8 / G) * (lane % G), nm, sc, z, nw_last, l3, l4);
+        else if (G == 2 || G == 4 || G == 8) {  // the last chunk's leaf lane / G, chains of this lane
+          if (ch == NCH - 1)
+            leaf = dm_leaf<FPM, (G == 2 || G == 4 || G == 8) ? 8 / G : 8>(img + (lane / G) * DM_S,
+                                                                       (8 / G) * (lane % G), nm, sc, z, nw_last, l3, l4);
+          else
+            leaf = dm_leaf<FPM>(img + lane * DM_S, 0, nm, sc, z, 16, l3, l4);
+        }
         else
           leaf = dm_leaf<FPM>(img + lane * DM_S, 0, nm, sc, z, ch < NCH - 1 ? 16 : nw_last, l3, l4);
         if (ch == NCH - 1) {
@@ -1091,21 +1145,28 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         a3 += l3;
         a4 += l4;
         // numpy's tree over the lane-ordered leaves (the tri form: two depths)
-        const double cs = (ch == NCH - 1 && G == 3) ? wave_sum_tri_split_f64(leaf)
+        const double cs = PAIR ? half_sum_f64(leaf)
+                          : (ch == NCH - 1 && G == 3) ? wave_sum_tri_split_f64(leaf)
                           : (ch == NCH - 1 && sh.tri) ? wave_sum_tri_f64(leaf) : wave_sum_f64(leaf);
         ssq = ch == 0 ? cs : ssq + cs;         // chunk sums in order (all scaled by 2^-102)
         wave_lds_sync();
       }
       ssq = __builtin_ldexp(ssq, 102);  // exact: numpy's sum of squared deviations
       if constexpr (FPM) {  // the fp64 d^3 / d^4 sums, parked as their two 32-bit halves
-        const uint64_t b3 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(a3, 153)));
-        const uint64_t b4 = (uint64_t)__double_as_longlong(wave_sum_f64(__builtin_ldexp(a4, 204)));
-        kT3l = mine ? (uint32_t)b3 : kT3l;
-        kT3h = mine ? (uint32_t)(b3 >> 32) : kT3h;
-        kT4l = mine ? (uint32_t)b4 : kT4l;
-        kT4h = mine ? (uint32_t)(b4 >> 32) : kT4h;
+        const double s3 = __builtin_ldexp(a3, 153), s4 = __builtin_ldexp(a4, 204);
+        const uint64_t b3 = (uint64_t)__double_as_longlong(PAIR ? half_sum_f64(s3) : wave_sum_f64(s3));
+        const uint64_t b4 = (uint64_t)__double_as_longlong(PAIR ? half_sum_f64(s4) : wave_sum_f64(s4));
+        park_u32(kT3l, (uint32_t)b3);
+        park_u32(kT3h, (uint32_t)(b3 >> 32));
+        park_u32(kT4l, (uint32_t)b4);
+        park_u32(kT4h, (uint32_t)(b4 >> 32));
       }
-      kssq = mine ? ssq : kssq;
+      if constexpr (PAIR) {
+        const double va = lane_f64(ssq, 0), vb = lane_f64(ssq, 32);
+        kssq = mine ? va : mine2 ? vb : kssq;
+      } else {
+        kssq = mine ? ssq : kssq;
+      }
     }
     // ---- finalise the batch: lane i -> row base + i
     if (lane < cnt) {
@@ -1356,6 +1417,10 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     // (PFE_OPT_LYON8_DM_SPLIT = 0 keeps one lane per leaf)
     const int G = !o.lyon8_dm_split ? 1
                   : dsh.tri ? 3  // the tri form's big leaf split by chains
+                  // two one-chunk rows per wave where a chain split would only halve the
+                  // leaves' work (32 leaves); at <= 16 the 4- and 8-lane splits are faster
+                  // (profiles/r05_lyon8_dm_pairs.txt)
+                  : (dnch == 1 && dsh.leaves_last > 16 && dsh.leaves_last <= 32 && o.lyon8_dm_split == 1) ? 16
                   : dsh.leaves_last <= 8 ? 8 : dsh.leaves_last <= 16 ? 4 : dsh.leaves_last <= 32 ? 2 : 1;
     if (o.lyon8_dm == 0 && dnch <= PFE_DM_FPM_MAXCH) {
 #define PFE_DMK(C)                                                                   \
@@ -1364,6 +1429,7 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     case 4: launch_dm_kernel<C, true, 4>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 2: launch_dm_kernel<C, true, 2>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 3: launch_dm_kernel<C, true, 3>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    case 16: if constexpr (C == 1) launch_dm_kernel<1, true, 16>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     default: launch_dm_kernel<C, true, 1>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
   }
       switch (dnch) {

@@ -18,7 +18,8 @@ struct Options {
   int pfd_waves = 4;               // waves per fold of the PFD dmprof kernel (4 or 1)
   int lyon8_dm = 0;                // DataBlock DM rows (pfe.h PFE_OPT_LYON8_DM, 0..2)
   int pfd_split = 0;               // PFD dmprof: 1 part sums by k_pfd_parts beside the sweep, 0 fused
-  int lyon8_dm_split = 1;          // DataBlock rows: chain-split last chunks of <= 32 leaves
+  int lyon8_dm_split = 1;          // DataBlock rows: 1 split last chunks + paired one-chunk rows,
+                                   // 2 chain splits only, 0 one lane per leaf
 };
 
 }  // namespace pfe

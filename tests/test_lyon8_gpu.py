@@ -228,17 +228,22 @@ def test_long_dm_rows_golden_dmplane(engine):
 def test_long_dm_rows_split_last_chunk(engine, lp, ld):
     """Last numpy chunks of <= 32 leaves (nDM = 30, 72, 160, 8, 66, 80, 16, 193: 32, 8, 32, 8,
     2, 16, 16 and 1 leaves) summed by 2, 4 or 8 lanes per leaf, each with some of the leaf's 8
-    chains, and the tri form (nDM = 33, 97, 225) with its 128-byte leaves split over the
-    quad's idle lane (round 5, PFE_OPT_LYON8_DM_SPLIT): mean and std bit-identical to one lane per leaf
-    and bit-exact against the oracle; skew / kurt (their d^3 / d^4 sums are grouped by lane, in
-    any order) within 1e-12 of one lane per leaf."""
-    prof, dm = lyon_batch(300, lp, ld, seed=5 + ld + lp, adversarial=True)
-    got = engine.lyon8(prof, dm)
+    chains, the tri form (nDM = 33, 97, 225) with its 128-byte leaves split over the quad's
+    idle lane, and one-chunk rows of <= 32 leaves (nDM = 30, 8, 16) two per wave (round 5,
+    PFE_OPT_LYON8_DM_SPLIT 1; 2 = the chain splits only): mean and std bit-identical to one
+    lane per leaf and bit-exact against the oracle; skew / kurt (their d^3 / d^4 sums are
+    grouped by lane, in any order) within 1e-12 of one lane per leaf.  An odd row count and a
+    one-block grid (several 64-row batches per wave, a lone last row) cover the pairs' edges."""
+    prof, dm = lyon_batch(301, lp, ld, seed=5 + ld + lp, adversarial=True)
     with engine.options(lyon8_dm_split=0):
         one = engine.lyon8(prof, dm)
-    for c in (0, 1, 4, 5):
-        assert np.array_equal(got[:, c].view(np.uint64), one[:, c].view(np.uint64))
-    m = ~np.isnan(one)
-    assert np.array_equal(np.isnan(got), np.isnan(one))
-    assert (np.abs(got - one)[m] / np.maximum(1, np.abs(one[m]))).max() <= TOL
-    check(got, lyon8_batched(prof, dm), exact_cols=(0, 1, 4, 5))
+    ref = lyon8_batched(prof, dm)
+    for opts in ({}, {"lyon8_dm_split": 2}, {"lyon8_blocks": 1}):
+        with engine.options(**opts):
+            got = engine.lyon8(prof, dm)
+        for c in (0, 1, 4, 5):
+            assert np.array_equal(got[:, c].view(np.uint64), one[:, c].view(np.uint64)), (opts, c)
+        m = ~np.isnan(one)
+        assert np.array_equal(np.isnan(got), np.isnan(one))
+        assert (np.abs(got - one)[m] / np.maximum(1, np.abs(one[m]))).max() <= TOL
+        check(got, ref, exact_cols=(0, 1, 4, 5))
