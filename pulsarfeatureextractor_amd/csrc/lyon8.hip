@@ -920,19 +920,22 @@ __device__ __forceinline__ double wave_sum_tri_split_f64(double v) {
 // Sums over each 32-lane half of the wave (two rows per wave, G == 16 of lyon8_u8_dm): the
 // in-row DPP steps of wave_sum_* and one exchange with lane ^ 16 -- for 32 leaves numpy's
 // (tree of 0..15) + (tree of 16..31), for fewer the rows past them add +0.0
+// (the exchange between the two DPP rows of a half is a v_permlane16_swap per dword, not a
+// ds_bpermute: every lane of the row pair adds even row + odd row, the same bits)
 __device__ __forceinline__ uint32_t half_sum_u32(uint32_t v) {
   v += (uint32_t)dpp_i32<DPP_QUAD_XOR1>((int)v);
   v += (uint32_t)dpp_i32<DPP_QUAD_XOR2>((int)v);
   v += (uint32_t)dpp_i32<DPP_ROW_HALF_MIRROR>((int)v);
   v += (uint32_t)dpp_i32<DPP_ROW_MIRROR>((int)v);
-  return v + (uint32_t)__shfl_xor((int)v, 16);
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return a[0] + a[1];
 }
 __device__ __forceinline__ double half_sum_f64(double v) {
   v += dpp_f64<DPP_QUAD_XOR1>(v);
   v += dpp_f64<DPP_QUAD_XOR2>(v);
   v += dpp_f64<DPP_ROW_HALF_MIRROR>(v);
   v += dpp_f64<DPP_ROW_MIRROR>(v);
-  return v + __shfl_xor(v, 16);
+  return swap16_sum(v);
 }
 
 // write chunk ch of the row (its pieces q[8ch .. 8ch+7]) into the wave's LDS image.  Full
