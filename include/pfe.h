@@ -67,7 +67,11 @@ extern "C" {
                                         is at most 510 n^(1/3); or, in pfe_bates22, a
                                         sub-band shape beyond nsub 65536 x nBins 16384 --
                                         the other groups' scores are still computed).  The
-                                        row is not scored */
+                                        row is not scored.  pfe_bates22 refuses the whole
+                                        call (PFE_EINVAL) when nsub * nBins > 2^24 bytes
+                                        per candidate, so the per-row mark is reached by
+                                        nsub > 65536 with nBins < 256 or nBins > 16384
+                                        with nsub < 1024 */
 #define PFE_ST_DGF_INDEXERROR 0x100u /* informational: double-Gaussian IndexError path taken,
                                         s10=s11=1e6 (ProfileOperations.py:762-764) */
 #define PFE_ST_FAIL_MASK      0x0FFu

@@ -508,7 +508,9 @@ static int check_bates_in(pfe_handle* h, const pfe_bates_in* in, const char* fn,
     return set_err(h, PFE_EINVAL, "%s: lp=%d outside [%d,%d]", fn, in->lp, need_dm ? 8 : 1,
                    need_dm ? 1024 : 16384);
   // pfe_subband3 computes nothing else, so an unsupported sub-band shape fails the call; in
-  // pfe_bates22 it only fails the rows' sub-band group (PFE_ST_UNSUPPORTED per row)
+  // pfe_bates22 it only fails the rows' sub-band group (PFE_ST_UNSUPPORTED per row), within
+  // the per-candidate bound of 2^24 sub-band bytes that pfe_bates22 itself checks (pfe.h
+  // PFE_ST_UNSUPPORTED)
   if (!need_dm) {
     if (const char* why = pfe::subband_shape_error(in->nsub, in->lsb))
       return set_err(h, PFE_EINVAL, "%s: sub-band shape %dx%d: %s", fn, in->nsub, in->lsb, why);

@@ -116,8 +116,23 @@ def parse(path: str, superb: bool | None = None) -> PHCXCandidate:
     names containing '.gz' are HTRU PHCX (section 1), anything else SUPERB (section 0)."""
     if superb is None:
         superb = ".gz" not in path
-    root = _read_xml(path, superb)
-    sec = 0 if superb else 1
+    return _from_root(_read_xml(path, superb), 0 if superb else 1, path)
+
+
+def parse_document(doc, section: int) -> PHCXCandidate:
+    """A candidate from the XML the reference's own objects hold: the minidom Document that
+    PHCXFile.load keeps in self.rawdata and hands to PHCXOperations (PHCXFile.py:103-104,
+    :454-654), or its text / bytes; `section` is the reference's argument (1 HTRU PHCX, 0
+    SUPERB), which selects the k-th occurrence of every tag as getElementsByTagName(tag)[k]
+    does."""
+    if hasattr(doc, "toxml"):
+        doc = doc.toxml(encoding="utf-8")
+    root = ET.fromstring(doc)
+    return _from_root(root, int(section), "")
+
+
+def _from_root(root, sec: int, path: str) -> PHCXCandidate:
+    superb = sec == 0
 
     def elems(tag):
         return list(root.iter(tag))

@@ -64,12 +64,18 @@ def _walk_matches(top: str, ft: str, chunk: int = 2048):
             continue
         with it:
             names = []
+            failed = False
             while True:
                 try:
                     e = next(it)
                 except StopIteration:
                     break
                 except OSError:
+                    # os.walk drops the whole directory (its files and subdirectories) when
+                    # listing fails partway; chunks already yielded from it cannot be taken
+                    # back (a documented divergence: only a directory of > `chunk` entries
+                    # that fails after its first chunk differs)
+                    failed = True
                     break
                 try:
                     is_dir = e.is_dir()
@@ -84,6 +90,8 @@ def _walk_matches(top: str, ft: str, chunk: int = 2048):
                         names = []
                         if hit:
                             yield hit
+            if failed:
+                continue
             hit = [pre + n for n in names if match(n)]
             if hit:
                 yield hit
@@ -113,7 +121,8 @@ class PathFeed:
     order, the first `skip` dropped) while the first batches are already parsed: _stream
     takes a batch as soon as its paths are listed, so the walk of a large directory overlaps
     the parsing instead of preceding it.  Reads block until the paths they need are listed;
-    len() waits for the whole walk.  on_done(total, skipped) runs on the walk thread."""
+    len() waits for the whole walk.  on_done(total, skipped) runs on the walk thread, before
+    the walk is marked done."""
 
     def __init__(self, gen=None, skip=0, on_done=None, paths=None):
         self._paths = list(paths) if paths is not None else []
@@ -135,14 +144,16 @@ class PathFeed:
                 with self._cv:
                     self._paths.extend(hit)
                     self._cv.notify_all()
+            # before the walk reports done: a reader waiting on len() (the run summary) sees
+            # on_done's metric and log line first
+            if on_done is not None:
+                on_done(seen, min(seen, skip))
         except BaseException as e:  # re-raised to the reader
             self._err = e
         finally:
             with self._cv:
                 self._done = True
                 self._cv.notify_all()
-        if on_done is not None and self._err is None:
-            on_done(seen, min(seen, skip))
 
     def wait(self, n):
         """Block until n paths are listed or the walk is over; -> the number listed (<= n)."""
@@ -950,8 +961,10 @@ class DataProcessor:
                 res.err[i] = GROUP_ERRORS[0][1]
             elif mode == "lyon8":
                 res.mat[i, :4] = np.nan
-            else:  # profile mode: computeProfileScores of the empty profile
-                res.rows[i] = np.zeros(0)
+            else:  # profile mode: load() already filled scores with numberOfScores (22) NaNs
+                # (PHCXFile.py:115-118, SUPERBPHCXFile.py:114-117) and computeProfileScores
+                # (:301-304) appends the empty profile to that list
+                res.rows[i] = np.full(22, np.nan)
 
     def _stream_text(self, paths, mode, out_path, style, run):
         """Collective modes: stream parse -> score, append each batch's lines (pfe_format_rows,

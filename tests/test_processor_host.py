@@ -285,6 +285,19 @@ def test_verbose_runs_the_reference_validity_checks(tmp_path, monkeypatch):
             assert rows[bad][:4] == ["0"] * 4 and rows[bad][4:] != ["0"] * 4
         else:
             assert rows[bad][:4] != ["0"] * 4
+        # profile mode: load()'s 22 NaN scores plus the empty profile (PHCXFile.py:115-118,
+        # :301-304), i.e. 22 NaNs written as "0" (DataProcessor.py:423) for the invalid file,
+        # its 128 profile bins without -v
+        dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=logs.append, batch=4)
+        dp._slabs = PlainSlabs()
+        outp = str(tmp_path / f"p{int(verbose)}.csv")
+        dp.processPHCXCollectively(str(d) + "/", verbose, outp, False, True, False)
+        rows = {ln.split(",")[0]: ln.split(",")[1:] for ln in open(outp).read().splitlines()}
+        if verbose:
+            assert rows[bad] == ["0"] * 22, rows[bad]
+        else:
+            assert len(rows[bad]) == 128
+        assert all(len(rows[g]) == 128 for g in good)
     assert any("Invalid PHCX candidate" in str(m) for m in logs)
 
 
