@@ -266,26 +266,10 @@ def cpu_baseline_subband(lsb, sample):
 
 
 def pfd_block(n, shape, seed):
-    """n synthetic PRESTO folds of one shape -> pfe_pfd_dmprof inputs (numpy)."""
-    import numpy as np
+    """n synthetic PRESTO folds of one shape -> pfe_pfd_dmprof inputs (synth.pfd_fold_block)."""
+    from pulsarfeatureextractor_amd.synth import pfd_fold_block
 
-    from pulsarfeatureextractor_amd import pfd as _pfd
-    from pulsarfeatureextractor_amd.synth import pfd_candidate
-
-    npart, nsub, L = shape
-    datas = []
-    for i in range(n):
-        c = pfd_candidate(np.random.default_rng(seed + i), npart, nsub, L)
-        chanpersub = c["numchan"] // nsub
-        sd = c["chan_wid"] * chanpersub
-        stats = c["stats"]
-        datas.append(_pfd.PFDData(
-            npart=npart, nsub=nsub, proflen=L, profs=c["profs"], bestdm=c["bestdm"],
-            binspersec=c["fold_p1"] * L, avgprof=(c["profs"] / L).sum(),
-            varprof=float(stats[:, :, 5].sum()), dms=c["dms"], numdms=len(c["dms"]),
-            bary_p1=c["fold_p1"],
-            subfreqs=np.arange(nsub, dtype="d") * sd + (c["lofreq"] + sd - c["chan_wid"])))
-    return datas
+    return pfd_fold_block(n, shape, seed)
 
 
 def cpu_baseline_pfd(shape, sample):

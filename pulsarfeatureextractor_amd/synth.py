@@ -136,3 +136,25 @@ def pfd_candidate(rng: np.random.Generator, npart: int = 8, nsub: int = 16, prof
     dms = np.linspace(bestdm - rng.uniform(5, 30), bestdm + rng.uniform(5, 30), ndms)
     return dict(profs=profs, stats=stats, dms=dms, bestdm=bestdm, fold_p1=f1,
                 bary_p1=1.0 / f1, lofreq=lofreq, chan_wid=chan_wid, numchan=numchan)
+
+
+def pfd_fold_block(n: int, shape, seed: int):
+    """n synthetic PRESTO folds of one (npart, nsub, proflen) shape as pfd.PFDData records
+    (what pfd.read returns for the files pfd.write would make of them): bench.py's PFD
+    workload, fold i drawn from default_rng(seed + i)."""
+    from . import pfd as _pfd
+
+    npart, nsub, L = shape
+    datas = []
+    for i in range(n):
+        c = pfd_candidate(np.random.default_rng(seed + i), npart, nsub, L)
+        chanpersub = c["numchan"] // nsub
+        sd = c["chan_wid"] * chanpersub
+        stats = c["stats"]
+        datas.append(_pfd.PFDData(
+            npart=npart, nsub=nsub, proflen=L, profs=c["profs"], bestdm=c["bestdm"],
+            binspersec=c["fold_p1"] * L, avgprof=(c["profs"] / L).sum(),
+            varprof=float(stats[:, :, 5].sum()), dms=c["dms"], numdms=len(c["dms"]),
+            bary_p1=c["fold_p1"],
+            subfreqs=np.arange(nsub, dtype="d") * sd + (c["lofreq"] + sd - c["chan_wid"])))
+    return datas

@@ -139,6 +139,56 @@ def test_config2_full_size_10m(engine):
     torch.cuda.empty_cache()
 
 
+def test_phcx_ndm120_full_size_1m(engine):
+    """The benched real-PHCX shape at the size bench.py times (extra.lyon8_phcx_ndm120): one
+    lyon8_u8_dm launch over 1M resident candidates of a 128-byte profile and a 120 x 128-byte
+    DataBlock row (15 360 bytes), on bench.py's rows themselves (generator and seed):
+      * the profile's mean and std and the DataBlock row's mean bit-exact on EVERY row (byte
+        sums are exact, so numpy's x.sum() / L is the correctly rounded quotient; the 128-byte
+        profile's centred squares sum exactly as well) -- computed here with torch in fp64;
+      * all 8 features of 600 rows drawn from the last 100k against the oracle, mean/std of
+        both rows bit-exact (the DataBlock std follows numpy's 8192-element chunks);
+      * a 4096-row block tiled to 1M rows: every tile bit-identical to the first, the first
+        200 rows against the oracle (a grid-stride or 32-bit offset fault past 2^31 bytes of
+        DataBlock rows -- 140k rows -- breaks that)."""
+    import torch
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    n, ld = 1_000_000, 15360
+    tp, td = lyon_batch_torch(n, 128, ld, seed=20261023)   # bench.py run_lyon8_phcx(ld=15360)
+    out = engine.lyon8(tp, td)
+    engine.synchronize()
+    for s in range(0, n, 1 << 17):
+        x = tp[s:s + (1 << 17)].to(torch.float64)
+        mean = x.sum(dim=1) / 128.0
+        std = torch.sqrt(((x - mean[:, None]) ** 2).sum(dim=1) / 128.0)
+        d = td[s:s + (1 << 17)].to(torch.float64).sum(dim=1) / float(ld)
+        o = out[s:s + (1 << 17)]
+        assert torch.equal(o[:, 0], mean), f"profile mean, rows {s}.."
+        assert torch.equal(o[:, 1], std), f"profile std, rows {s}.."
+        assert torch.equal(o[:, 4], d), f"DataBlock mean, rows {s}.."
+    idx = torch.randint(n - 100_000, n, (600,), generator=torch.Generator().manual_seed(11))
+    check(out[idx].cpu().numpy(), lyon8_batched(tp[idx].cpu().numpy(), td[idx].cpu().numpy()))
+    del out, tp, td
+    torch.cuda.empty_cache()
+    blk = 4096
+    bp, bd = lyon_batch_torch(blk, 128, ld, seed=20261024)
+    reps = (n + blk - 1) // blk
+    tp = bp.repeat(reps, 1)[:n].contiguous()
+    td = bd.repeat(reps, 1)[:n].contiguous()
+    out = engine.lyon8(tp, td)
+    engine.synchronize()
+    ob = out.view(torch.int64)
+    full = (n // blk) * blk
+    tiles = ob[:full].view(-1, blk, 8)
+    bad = (tiles != tiles[:1]).any(dim=2).any(dim=1)
+    assert not bool(bad.any()), f"tiles differing from tile 0: {torch.nonzero(bad)[:10].flatten().tolist()}"
+    assert torch.equal(ob[full:], ob[: n - full])
+    check(out[:200].cpu().numpy(), lyon8_batched(bp[:200].cpu().numpy(), bd[:200].cpu().numpy()))
+    del out, ob, tiles, tp, td
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("lp,ld", [(128, 15360), (128, 16384), (64, 7680), (256, 8192),
                                    (128, 12800), (128, 8320), (64, 384), (256, 10240),
                                    (64, 16384), (256, 16384), (128, 8192), (64, 8192),

@@ -156,3 +156,39 @@ def test_batch_independence_and_device(engine, tmp_path):
     o, s = engine.pfd_bates22(*t)
     engine.synchronize()
     assert same(o.cpu().numpy(), full)
+
+
+def test_bench_size_131072_folds(engine):
+    """The 22-score PFD launch at the size bench.py times (--path pfd22): 131 072 folds of
+    16 x 32 x 128 (64 GB of fp64 folds resident), bench.py's 1024-fold block (seed 20261019)
+    tiled.  Every 1024-fold tile's scores and status bit-identical to the first (a fit does
+    not depend on its pool, and a grid-stride or 32-bit offset fault past 4 GB of folds would
+    break that); the first 48 folds against the oracle under this file's bar."""
+    import torch
+    from pulsarfeatureextractor_amd.synth import pfd_fold_block
+
+    n, blk = 131072, 1024
+    datas = pfd_fold_block(blk, (16, 32, 128), 20261019)
+    profs, sf, sc = pfd.batch_inputs(datas)
+    reps = n // blk
+
+    def tile(a):
+        t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        return t.repeat((reps,) + (1,) * (t.dim() - 1)).contiguous()
+
+    tp, tf, ts = tile(profs), tile(sf), tile(sc)
+    del profs
+    out, st = engine.pfd_bates22(tp, tf, ts)
+    engine.synchronize()
+    del tp, tf, ts
+    ob = out.view(torch.int64).view(reps, blk, 22)
+    bad = (ob != ob[:1]).any(dim=2).any(dim=1)
+    assert not bool(bad.any()), f"tiles differing from tile 0: {torch.nonzero(bad)[:10].flatten().tolist()}"
+    stt = st.view(reps, blk)
+    assert bool((stt == stt[:1]).all())
+    sub = datas[:48]
+    ref, ok, floor = oracle_floor(sub)
+    check(out[:48].cpu().numpy(), st[:48].cpu().numpy().view(np.uint32), ref, ok,
+          "131072 folds, tile 0", floor)
+    del out, st, ob
+    torch.cuda.empty_cache()

@@ -214,3 +214,51 @@ def test_subband_shape_beyond_every_kernel_fails_rows_not_call(engine):
     assert np.array_equal(o[:, :19], ref[:, :19], equal_nan=True)
     with pytest.raises(PfeError):
         engine.subband3(b["prof"], big, b["scal"])
+
+
+def test_config4_full_size_1m(engine):
+    """BASELINE config 4 at the size it names and bench.py times (extra.config4): one
+    pfe_subband3 launch over 1M resident candidates of a 256-bin profile and 16 x 256
+    sub-bands, on device pointers.
+      * bench.py's rows (its 16384-row block, seed 20261021, tiled to 1M): every tile's scores
+        and status bit-identical to the first; the first 100 rows against the oracle;
+      * a fresh (untiled) 1M batch generated on the device: 200 rows drawn from the last
+        100k against the oracle, s20 and s22 bit-exact, s21 within 1e-9."""
+    import torch
+    from pulsarfeatureextractor_amd.synth import lyon_batch_torch
+
+    n, blk, lsb = 1_000_000, 16384, 256
+    base = bates_batch(blk, lp=lsb, nsub=16, lsb=lsb, seed=20261021)   # bench.py tile_bates
+    reps = (n + blk - 1) // blk
+    t = {k: torch.from_numpy(np.ascontiguousarray(base[k])).cuda() for k in ("prof", "sub", "scal")}
+    bt = {k: v.repeat((reps,) + (1,) * (v.dim() - 1))[:n].contiguous() for k, v in t.items()}
+    out, st = engine.subband3(bt["prof"], bt["sub"], bt["scal"])
+    engine.synchronize()
+    full = (n // blk) * blk
+    ob = out.view(torch.int64)
+    tiles = ob[:full].view(-1, blk, 3)
+    bad = (tiles != tiles[:1]).any(dim=2).any(dim=1)
+    assert not bool(bad.any()), f"tiles differing from tile 0: {torch.nonzero(bad)[:10].flatten().tolist()}"
+    assert torch.equal(ob[full:], ob[: n - full])
+    stt = st[:full].view(-1, blk)
+    assert bool((stt == stt[:1]).all()) and torch.equal(st[full:], st[: n - full])
+    ref, ok = oracle_sub(base["prof"][:100], base["sub"][:100], base["scal"][:100])
+    check(out[:100].cpu().numpy(), st[:100].cpu().numpy().view(np.uint32), ref, ok,
+          "config4 tile 0", lsb)
+    del out, st, ob, tiles, bt, t
+    torch.cuda.empty_cache()
+    prof, rows = lyon_batch_torch(n, lsb, 16 * lsb, seed=20261025)
+    sub = rows.view(n, 16, lsb)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(20261026)
+    scal = torch.zeros((n, 8), dtype=torch.float64, device="cuda")
+    scal[:, 3] = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) * 0.08 + 0.02
+    out, st = engine.subband3(prof, sub, scal)
+    engine.synchronize()
+    idx = torch.randint(n - 100_000, n, (200,), generator=torch.Generator().manual_seed(13))
+    pi, si, ci = (x[idx].cpu().numpy() for x in (prof, sub, scal))
+    ref, ok = oracle_sub(pi, si, ci)
+    check(out[idx].cpu().numpy(), st[idx].cpu().numpy().view(np.uint32), ref, ok,
+          "config4 fresh", lsb)
+    del out, st, prof, rows, sub, scal
+    torch.cuda.empty_cache()
