@@ -2,7 +2,7 @@
 
   python -m pulsarfeatureextractor_amd.cli -c <dir|file> -o <out> [--phcx|--superb]
          [--arff] [--profile] [--dmprof] [-v] [--device N] [--workers K] [--start K]
-         [--metrics FILE]
+         [--metrics FILE] [--gpus N [--devices D0,D1,...]]
 
 Same flags, same output-file probing (:147-160), same mode dispatch (:215-290), for PHCX,
 SUPERB and PFD files in every mode, --label included (its prompt is commented out in the
@@ -31,6 +31,11 @@ def main(argv=None):
     p.add_option("--dmprof", action="store_true", dest="dmprof", default=False)
     p.add_option("--device", action="store", dest="device", type="int", default=0)
     p.add_option("--workers", action="store", dest="workers", type="int", default=None)
+    # multi-GPU (not in the reference): N worker processes, one GPU each, over N contiguous
+    # shards of the discovered candidates; outputs concatenated in discovery order
+    p.add_option("--gpus", action="store", dest="gpus", type="int", default=1)
+    # the GPU of each worker, e.g. "0,1,2,3" (default: worker r on GPU r % visible GPUs)
+    p.add_option("--devices", action="store", dest="devices", type="string", default=None)
     # resume offset (not in the reference): skip the first K discovered candidates, e.g. the
     # ones a stopped collective run had already appended to its output file
     # (collective modes also keep <output>.progress = the --start value that resumes after
@@ -56,11 +61,15 @@ def main(argv=None):
         single, search = True, args.candDir
     else:
         search = ""
-    from .candidate import get_engine
+    devices = [int(d) for d in args.devices.split(",")] if args.devices else None
+    if args.gpus <= 1:
+        from .candidate import get_engine
 
-    get_engine(args.device)
+        get_engine(devices[0] if devices else args.device)
+    # else: the parent never initialises a GPU -- each shard worker is a spawned process that
+    # opens its own device (processor.DataProcessor._run_shards)
     dp = processor.DataProcessor(args.verbose, workers=args.workers, start=args.start,
-                                 metrics_path=args.metrics)
+                                 metrics_path=args.metrics, gpus=args.gpus, devices=devices)
     phcx, pfd, superb = args.phcx, args.pfd, args.superb
     try:
         if args.label:  # :220-225 (labelPFD with the two arguments ScoreGenerator passes)

@@ -103,7 +103,14 @@ static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
 // fit slots per wave of k_gdg8g: its SIMT phase (lmpar, one slot per lane) is the largest
 // share of the 8-parameter kernel, which runs one wave per SIMD (registers), so 48 slots
 // fill more lanes there; the LDS state (BlmState<8, 48>, 35 KB) still admits 4 waves per CU
-constexpr int GDG8_FPW = 48;
+#ifndef PFE_GDG8_FPW
+#define PFE_GDG8_FPW 48
+#endif
+constexpr int GDG8_FPW = PFE_GDG8_FPW;
+// waves per SIMD k_gdg8g is compiled for (its registers: 1)
+#ifndef PFE_GDG8_WPE
+#define PFE_GDG8_WPE 1
+#endif
 // fit slots per wave of the 4-parameter pooled kernels k_gt1g / k_gdgg up to 128 bins (two
 // waves per SIMD: BlmState<4, 44> + slot table + peel rows = 19 KB, 8 waves = 153 KB of LDS
 // per CU; their SIMT phase also runs one slot per lane)

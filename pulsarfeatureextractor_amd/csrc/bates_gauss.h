@@ -2261,7 +2261,7 @@ struct Gdg8Prob {
 };
 
 template <int P>
-__global__ __launch_bounds__(64) void k_gdg8g(BatesArgs a) {
+__global__ __launch_bounds__(64, PFE_GDG8_WPE) void k_gdg8g(BatesArgs a) {
   constexpr int FPW = GDG8_FPW;
   // 16 lanes (8 rows each) at 128 bins: 32 lanes measured 7 % slower there
   // (profiles/r02_gdg8_g32_ab.txt); 32 lanes (8 rows each) at 256 bins

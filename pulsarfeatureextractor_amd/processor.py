@@ -585,6 +585,7 @@ class RunMetrics:
         self.stage = {}  # finer host timers of the GPU stage (pack, gpu), summed over slots
         self.batches = 0
         self.reasons = {}
+        self.shards = []  # --gpus N: one entry per worker (merge)
         # the pipeline's slot threads add to the same timers concurrently
         self._lock = threading.Lock()
 
@@ -615,6 +616,25 @@ class RunMetrics:
                     self.score_s += dt
         return wrapped
 
+    def merge(self, m, rank, n, device):
+        """Fold one --gpus shard's metrics (its worker's finish()) into this run's: batches,
+        failures by reason, the parser / GPU-stage timers summed over the workers (host
+        seconds, as over the slots of one process), plus a per-shard entry."""
+        if not m:
+            return
+        with self._lock:
+            self.batches += m.get("batches", 0)
+            for k, v in m.get("failures_by_reason", {}).items():
+                self.reasons[k] = self.reasons.get(k, 0) + v
+            self.parse_s += m.get("parse_s", 0.0)
+            self.score_s += m.get("score_s", 0.0)
+            for k, v in m.items():
+                if k.endswith("_s") and k[:-2] in ("pack", "gpu", "emit", "discover"):
+                    self.stage[k[:-2]] = self.stage.get(k[:-2], 0.0) + v
+            self.shards.append({"rank": rank, "device": int(device), "candidates": int(n),
+                                "wall_s": m.get("wall_s"),
+                                "candidates_per_s": m.get("candidates_per_s")})
+
     def batch(self, res):
         self.batches += 1
         for e in res.err:
@@ -635,7 +655,8 @@ class RunMetrics:
                 **({"parse_head_s": round(self.parse_span[0], 6),
                     "parse_idle_s": round(self.parse_span[1] - self.parse_span[0] - self.parse_s, 6),
                     "parse_tail_s": round(wall - self.parse_span[1], 6)} if self.parse_span else {}),
-                **{k + "_s": round(v, 6) for k, v in sorted(self.stage.items())}}
+                **{k + "_s": round(v, 6) for k, v in sorted(self.stage.items())},
+                **({"shards": self.shards} if self.shards else {})}
 
 
 class DataProcessor:
@@ -647,8 +668,19 @@ class DataProcessor:
     """
 
     def __init__(self, debugFlag=False, engine=None, workers=None, log=print, batch=BATCH,
-                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True):
+                 start=0, gpu_batch=1 << 18, metrics_path=None, gpu_depth=2, ramp=True,
+                 gpus=1, devices=None, shard_engine=None, shard_slabs=None):
         self.debug = debugFlag
+        # --gpus N: the discovered paths are cut into N contiguous shards, each scored by its
+        # own worker process on its own GPU (own reader threads, pinned slabs, engine handles);
+        # the parent never touches a GPU and concatenates the shards' outputs in discovery
+        # order (_run_shards).  devices: the GPU of each worker (default rank % GPUs);
+        # shard_engine / shard_slabs: "module:callable" factories a worker builds its engine /
+        # slabs from instead of libpfe's (host tests)
+        self.gpus = max(1, int(gpus))
+        self.devices = list(devices) if devices else None
+        self.shard_engine, self.shard_slabs = shard_engine, shard_slabs
+        self._shard = None    # in a worker: (rank, suffix, its paths)
         self.verbose = False  # the entry point's verbose flag (-v): isValid per PHCX file
         self._run = None      # RunMetrics of the mode being run (stage timers)
         self.metrics_path = metrics_path
@@ -683,6 +715,8 @@ class DataProcessor:
     def _candidates(self, directory, regexes, single):
         """The run's candidate paths: a PathFeed whose walk runs beside the first batches'
         parsing for a directory, a list otherwise.  Run metrics "discover": the walk's time."""
+        if self._shard is not None:  # a worker: its shard of the parent's discovery
+            return list(self._shard[2])
         t0 = time.perf_counter()
         if directory == "":
             directory = os.path.dirname(os.path.realpath(__file__))
@@ -717,7 +751,7 @@ class DataProcessor:
     def _resuming(self, out_path):
         """A resumed run (start > 0) appends to the output the stopped run wrote: its ARFF
         header is already there, so a second one would break the file."""
-        return self.start > 0 and os.path.exists(out_path)
+        return self._shard is not None or (self.start > 0 and os.path.exists(out_path))
 
     def _fail(self, cand, why):
         self.log(f"Error reading profile data :\n\t{why}\n{cand}  did not have scores generated.")
@@ -736,6 +770,9 @@ class DataProcessor:
         return failed
 
     def _summary(self, processed, ok, failed, start, extra="", run=None):
+        if self._shard is not None:  # a worker: the parent reports the run
+            self.metrics = run.finish(processed, ok, failed) if run is not None else None
+            return
         end = datetime.datetime.now()
         self.log(f"\nCandidates processed:\t{processed}\nSuccesses:\t{ok}\nFailures:\t{failed}\n"
                  f"{extra}Execution time:  {end - start}")
@@ -1022,7 +1059,13 @@ class DataProcessor:
         run = RunMetrics(mode, self.start)
         self._run = run
         paths = self._candidates(directory, regexes, single)
-        ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0, run)
+        if self._sharding(single):
+            ok, failed = self._run_shards(
+                "processCollectively", (directory, verbose, regexes, outPath, arff,
+                                        genProfileData, single), paths, run, outs=[outPath],
+                out_arg=3)
+        else:
+            ok, failed = self._stream_text(paths, mode, outPath, 1 if arff else 0, run)
         self._summary(len(paths), ok, failed, start, run=run)
 
     def processPFDCollectively(self, directory, verbose, outPath, arff, genProfileData,
@@ -1050,6 +1093,11 @@ class DataProcessor:
         run = RunMetrics("separately", self.start)
         self._run = run
         paths = self._candidates(directory, regexes, single)
+        if self._sharding(single):
+            ok, failed = self._run_shards("processSeparately", (directory, verbose, regexes, single),
+                                          paths, run, outs=[])
+            self._summary(len(paths), ok, failed, start, run=run)
+            return
 
         from ._native import format_rows
 
@@ -1088,7 +1136,12 @@ class DataProcessor:
         run = RunMetrics("lyon8", self.start)
         self._run = run
         paths = self._candidates(directory, regexes, single)
-        ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0, run)
+        if self._sharding(single):
+            ok, failed = self._run_shards("dmprof", (directory, verbose, regexes, outPath, arff,
+                                                     single), paths, run, outs=[outPath],
+                                          out_arg=3)
+        else:
+            ok, failed = self._stream_text(paths, "lyon8", outPath, 1 if arff else 0, run)
         self._summary(len(paths), ok, failed, start, run=run)
 
     def dmprofPFD(self, directory, verbose, outPath, arff, processSingleCandidate):
@@ -1118,6 +1171,86 @@ class DataProcessor:
         self.processCollectively(directory, verbose, [PHCX_RE] + list(PFD_RES), outPath, arff,
                                  genProfileData, processSingleCandidate)
 
+    # ---- --gpus N: contiguous shards over worker processes ---------------------------
+    def _sharding(self, single):
+        return self.gpus > 1 and self._shard is None and not single
+
+    def _run_shards(self, entry, args, paths, run, outs, out_arg=None, progress=True):
+        """Score `paths` (the whole discovery, resume offset applied) as self.gpus contiguous
+        shards, one spawned worker process per shard (_shard_worker): worker r runs the same
+        entry point of a single-GPU DataProcessor on device devices[r] over its shard, writing
+        every output file, the error log and the progress marker with the suffix ".shard<r>".
+        The parent (which never initialises a GPU, so spawning is safe) then appends the
+        shards' files to the real ones in rank order -- the discovery order of a one-process
+        run, byte for byte -- removes them, and writes <out>.progress = start + len(paths).
+        Only a finished run is merged: a stopped run leaves its shard files and the previous
+        progress marker, so it resumes from --start as before."""
+        import multiprocessing as mp
+
+        paths = list(paths)
+        n, g = len(paths), self.gpus
+        cuts = [n * r // g for r in range(g + 1)]
+        devices = self.devices or _default_devices(g)
+        threads = max(1, self.workers // g)
+        ctx = mp.get_context("spawn")
+        procs, pipes = [], []
+        kw = {"debugFlag": self.debug, "workers": threads, "batch": self.batch,
+              "gpu_batch": self.gpu_batch, "gpu_depth": self.depth, "ramp": self.ramp}
+        flags = {"phcx": self.phcx, "pfd": self.pfd, "superb": self.superb}
+        for r in range(g):
+            sfx = f".shard{r}"
+            a = list(args)
+            if out_arg is not None:
+                a[out_arg] = a[out_arg] + sfx
+            rd, wr = ctx.Pipe(duplex=False)
+            p = ctx.Process(target=_shard_worker, name=f"pfe-shard{r}",
+                            args=(wr, kw, flags, entry, tuple(a), paths[cuts[r]:cuts[r + 1]], r,
+                                  sfx, int(devices[r % len(devices)]), self.shard_engine,
+                                  self.shard_slabs))
+            p.start()
+            wr.close()
+            procs.append(p)
+            pipes.append(rd)
+        results, errors = [], []
+        for r, (p, rd) in enumerate(zip(procs, pipes)):
+            try:
+                res = rd.recv()
+            except EOFError:
+                res = {"error": f"shard {r}: worker exited with code {p.exitcode}"}
+            p.join()
+            if res.get("error"):
+                errors.append(res["error"])
+            results.append(res)
+        if errors:
+            raise RuntimeError("sharded run failed:\n" + "\n".join(errors))
+        t0 = time.perf_counter()
+        for out in list(outs) + [self.candidateErrorLog]:
+            with open(out, "ab") as dst:
+                for r in range(g):
+                    part = out + f".shard{r}"
+                    if os.path.exists(part):
+                        with open(part, "rb") as src:
+                            while True:
+                                b = src.read(1 << 24)
+                                if not b:
+                                    break
+                                dst.write(b)
+                        os.remove(part)
+        for out in outs:
+            for r in range(g):
+                q = out + f".shard{r}.progress"
+                if os.path.exists(q):
+                    os.remove(q)
+        if progress and outs:
+            _write_progress(outs[0], self.start + n)
+        run.add("merge", time.perf_counter() - t0)
+        ok = failed = 0
+        for r, res in enumerate(results):
+            ok += res["ok"]
+            failed += res["failed"]
+            run.merge(res.get("metrics"), r, cuts[r + 1] - cuts[r], devices[r % len(devices)])
+        return ok, failed
+
     # ---- label mode (:691-826) --------------------------------------------------------
     def label(self, directory, verbose, regexes):
         """Scores.csv, Profile.csv, DMCurve.csv and Cands.meta in the candidate directory:
@@ -1129,13 +1262,21 @@ class DataProcessor:
         self.verbose = bool(verbose)
         if directory == "":
             directory = os.path.dirname(os.path.realpath(__file__))
-        meta = directory + "/Cands.meta"
-        files = {"scores": directory + "/Scores.csv", "profile": directory + "/Profile.csv",
-                 "dm": directory + "/DMCurve.csv"}
+        sfx = self._shard[1] if self._shard is not None else ""
+        meta = directory + "/Cands.meta" + sfx
+        files = {"scores": directory + "/Scores.csv" + sfx,
+                 "profile": directory + "/Profile.csv" + sfx, "dm": directory + "/DMCurve.csv" + sfx}
         start = datetime.datetime.now()
         run = RunMetrics("label", self.start)
         self._run = run
         paths = self._candidates(directory, regexes, False)
+        if self._sharding(False):
+            ok, failed = self._run_shards("label", (directory, verbose, regexes), paths, run,
+                                          outs=[files["scores"], files["profile"], files["dm"],
+                                                meta], progress=False)
+            self._summary(len(paths), ok, failed, start,
+                          f"Positive:\t{self.positive}\nNegative:\t{self.negative}\n", run=run)
+            return
         lab = "0"
         out = {k: [] for k in ("scores", "profile", "dm", "meta")}
 
@@ -1196,3 +1337,88 @@ def _as_matrix(res):
         if not e:
             mat[i] = r
     return mat, skip
+
+
+def _default_devices(g):
+    """rank r -> GPU r % (visible GPUs); counting devices does not initialise the GPU."""
+    try:
+        import torch
+
+        nd = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        nd = 0
+    return list(range(max(1, min(g, nd)))) if nd else [0]
+
+
+def _load_factory(spec):
+    import importlib
+
+    mod, _, fn = spec.partition(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def _bind_numa(device):
+    """Best effort: run this worker on the host CPUs of its GPU's NUMA node (sysfs), so its
+    reader threads and the first touch of its pinned slabs are node-local."""
+    try:
+        import torch
+
+        pr = torch.cuda.get_device_properties(device)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        if mine:
+            os.sched_setaffinity(0, mine)
+            return node
+    except Exception:  # noqa: BLE001
+        return None
+    return None
+
+
+def _shard_worker(conn, kw, flags, entry, args, paths, rank, suffix, device, engine_spec,
+                  slabs_spec):
+    """One shard of a --gpus N run (a spawned process): a single-GPU DataProcessor on
+    `device` over `paths`, its files suffixed; sends {"ok", "failed", "metrics"} back."""
+    import traceback
+
+    try:
+        if engine_spec:
+            engine = _load_factory(engine_spec)()
+        else:
+            from .candidate import set_engine
+            from ._native import Engine
+
+            _bind_numa(device)
+            engine = Engine(device)
+            set_engine(engine)
+        dp = DataProcessor(engine=engine, log=lambda *a: print(f"[shard {rank}]", *a), **kw)
+        if slabs_spec:
+            dp._slabs = _load_factory(slabs_spec)()
+        dp.candidateErrorLog = "CandidateErrorLog.txt" + suffix
+        for k, v in flags.items():
+            setattr(dp, k, v)
+        dp._shard = (rank, suffix, paths)
+        counts = {}
+        real = dp._summary
+
+        def capture(processed, ok, failed, start, extra="", run=None):
+            counts["ok"], counts["failed"] = ok, failed
+            real(processed, ok, failed, start, extra, run)
+
+        dp._summary = capture
+        getattr(dp, entry)(*args)
+        conn.send({"ok": counts.get("ok", 0), "failed": counts.get("failed", 0),
+                   "metrics": dp.metrics})
+    except BaseException:  # noqa: BLE001 -- reported to the parent
+        conn.send({"error": f"shard {rank}:\n" + traceback.format_exc()})
+    finally:
+        conn.close()

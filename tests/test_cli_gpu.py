@@ -167,3 +167,34 @@ def test_pipeline_slots_follow_the_callers_engine_options(tmp_path, monkeypatch)
                     assert slot.get_option(name) == e.get_option(name), name
         # both slots computed with the batched solver: the same text as one slot
         assert outs[1] == outs[2]
+
+
+@pytest.mark.parametrize("extra", [[], ["--dmprof", "--arff"]])
+def test_cli_two_gpu_shards_match_one(tmp_path, monkeypatch, extra):
+    """--gpus 2 with both shard workers on cuda:0 (--devices 0,0; the box has one GPU): two
+    spawned processes, each with its own engine, reader threads and pinned slabs, over the two
+    contiguous halves of the discovery.  Output text, error log and <out>.progress are
+    byte-identical to the one-process run (ARFF: but for the header's timestamp)."""
+    d = load("bates22_phcx128")
+    cands = str(tmp_path / "cands")
+    write_set(d, cands)
+    with open(os.path.join(cands, "zz_broken.phcx.gz"), "wb") as f:
+        f.write(b"not gzip")
+    got = {}
+    for g in ("1", "2"):
+        wd = tmp_path / f"w{g}"
+        wd.mkdir()
+        monkeypatch.chdir(wd)
+        out = str(wd / "out.txt")
+        open(out, "w").close()
+        args = ["-c", cands, "-o", out, "--phcx", "--workers", "2", "--gpus", g, *extra]
+        if g == "2":
+            args += ["--devices", "0,0"]
+        assert cli.main(args) == 0
+        got[g] = [open(p, "rb").read() for p in (out, "CandidateErrorLog.txt", out + ".progress")]
+        assert not [p for p in os.listdir(wd) if ".shard" in p]
+    a, b = got["1"], got["2"]
+    if extra:
+        a[0], b[0] = a[0].split(b"\n", 1)[1], b[0].split(b"\n", 1)[1]
+    assert a == b
+    assert a[1].count(b"\n") >= 1 and int(a[2]) == len(d["ok"]) + 1

@@ -399,3 +399,84 @@ def test_discover_streams_large_directories_in_os_walk_order(tmp_path):
             assert got == ref(d, pats) and len(got) > 3000
     chunks = list(processor.iter_discover(str(big), [processor.PHCX_RE]))
     assert len(chunks) >= 3  # streamed while the big directory is listed
+
+
+@pytest.mark.parametrize("mode", ["scores", "arff", "lyon8", "separately", "label"])
+def test_sharded_run_matches_one_process(tmp_path, monkeypatch, mode):
+    """--gpus N (DataProcessor(gpus=N)): the discovered paths in N contiguous shards, one
+    spawned worker process each, outputs appended in rank order.  The output text, the error
+    log, the .progress marker (and the label files / .dat files) are byte-identical to a
+    one-process run, with a resume offset too.  Workers build the stub engine and plain slabs
+    (shard_engine / shard_slabs) instead of libpfe's."""
+    import shutil
+
+    d0 = make_dir(tmp_path)
+    results = {}
+    wd = tmp_path / "run"
+    for g in (1, 3):   # the same paths for both runs: a fresh copy of the tree in one place
+        shutil.rmtree(wd, ignore_errors=True)
+        shutil.copytree(d0, wd / "cands")
+        monkeypatch.chdir(wd)
+        d = str(wd / "cands")
+        kw = dict(workers=2, log=lambda *a: None, batch=8, start=5)
+        if g > 1:
+            kw.update(gpus=g, shard_engine="test_processor_host:StubEngine",
+                      shard_slabs="test_processor_host:PlainSlabs")
+        dp = processor.DataProcessor(engine=StubEngine(), **kw)
+        dp._slabs = PlainSlabs()
+        out = str(wd / ("o.arff" if mode == "arff" else "o.csv"))
+        if mode in ("scores", "arff"):
+            dp.processPHCXCollectively(d + "/", False, out, mode == "arff", False, False)
+        elif mode == "lyon8":
+            dp.dmprofPHCX(d + "/", False, out, False, False)
+        elif mode == "separately":
+            dp.processPHCXSeparately(d + "/", False, False)
+        else:
+            dp.labelPHCX(d, False)
+        files = {}
+        for root, _dirs, names in os.walk(wd):
+            for nm in names:
+                p = os.path.join(root, nm)
+                files[os.path.relpath(p, wd)] = open(p, "rb").read()
+        assert not any(".shard" in k for k in files), sorted(files)
+        results[g] = (files, dp.metrics)
+    f1, m1 = results[1]
+    f3, m3 = results[3]
+    assert sorted(f1) == sorted(f3)
+    for k in f1:
+        a, b = f1[k], f3[k]
+        if k.endswith(".arff"):  # "@relation PulsarCandidates_<now>": the run's timestamp
+            assert a.split(b"\n", 1)[0][:27] == b.split(b"\n", 1)[0][:27]
+            a, b = a.split(b"\n", 1)[1], b.split(b"\n", 1)[1]
+        assert a == b, k
+    assert len(f1["CandidateErrorLog.txt"]) > 0
+    for key in ("candidates", "successes", "failures", "failures_by_reason"):
+        assert m1[key] == m3[key], key
+    assert [s["rank"] for s in m3["shards"]] == [0, 1, 2]
+    assert sum(s["candidates"] for s in m3["shards"]) == m1["candidates"]
+
+
+def test_cli_gpus_flag_parses_devices(tmp_path, monkeypatch):
+    """The CLI's --gpus / --devices reach the DataProcessor, and with --gpus > 1 the parent
+    does not open an engine (the workers do)."""
+    from pulsarfeatureextractor_amd import candidate, cli
+
+    seen = {}
+
+    class Probe(processor.DataProcessor):
+        def __init__(self, *a, **k):
+            seen.update(k)
+            super().__init__(*a, **k)
+
+        def processPHCXCollectively(self, *a):
+            seen["called"] = True
+
+    monkeypatch.setattr(processor, "DataProcessor", Probe)
+    monkeypatch.setattr(candidate, "get_engine", lambda *a: (_ for _ in ()).throw(AssertionError("engine opened")))
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "c").mkdir()
+    out = str(tmp_path / "o.csv")
+    open(out, "w").close()
+    assert cli.main(["-c", str(tmp_path / "c"), "-o", out, "--phcx", "--gpus", "2",
+                     "--devices", "0,0"]) == 0
+    assert seen["gpus"] == 2 and seen["devices"] == [0, 0] and seen["called"]
