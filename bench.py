@@ -32,6 +32,9 @@ Besides the contract fields the JSON line carries:
                               check that every 16384-row tile of the tiled batch scored
                               bit-identically to the first
                    config4 -- pfe_subband3 over 1M candidates of 16 x 256 sub-bands
+                   config1 -- 1 000 candidates of 64 + 64 bins: the CPU NumPy loop it names
+                              (1 core) beside pfe_lyon8_u8 on the same rows (resident and
+                              from host arrays), with a parity check
                    config2_e2e -- config 2 end to end from pinned host memory (PCIe H2D of
                                   the rows + kernel + D2H of the features, pipelined), with
                                   the measured H2D bandwidth of the box
@@ -467,6 +470,67 @@ def run_lyon8(ctx, args, n, lp):
     }, out
 
 
+def run_config1(ctx, n=1000, lp=64, ld=64, steps=200, warmup=20):
+    """BASELINE config 1 as worded: 1k synthetic candidates, 64-bin profile + 64-bin DM
+    curve, 8 Lyon features.  Its named path is the reference's CPU NumPy loop, timed here on
+    one host core through the oracle (the reference-equivalent numpy/scipy loop, kind
+    "port"); beside it the same 1 000 rows through pfe_lyon8_u8 on the GPU, resident (the
+    launch-bound single step) and from host numpy arrays (DMA in and out per call), with
+    the GPU's features checked against the oracle's on every row (mean / std bit-exact)."""
+    import warnings
+
+    import numpy as np
+
+    from oracle.lyon import lyon8
+    from pulsarfeatureextractor_amd.synth import lyon_batch
+
+    torch = ctx.torch
+    prof, dm = lyon_batch(n, lp, ld, seed=20261027)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        lyon8(prof[:20], dm[:20])
+        t0 = time.perf_counter()
+        ref = lyon8(prof, dm)
+        cpu_s = time.perf_counter() - t0
+    tp, td = torch.from_numpy(prof).to(ctx.dev), torch.from_numpy(dm).to(ctx.dev)
+    out = torch.empty((n, 8), dtype=torch.float64, device=ctx.dev)
+
+    def step():
+        ctx.eng.lyon8(tp, td, out=out)
+
+    elapsed, kern_ms, _ = ctx.time_steps(step, steps, warmup)
+    got = out.cpu().numpy()
+    host = np.empty((n, 8))
+    ctx.eng.lyon8(prof, dm, out=host)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.eng.lyon8(prof, dm, out=host)
+    host_s = (time.perf_counter() - t0) / steps
+    m = ~np.isnan(ref)
+    exact = all(np.array_equal(got[m[:, c], c], ref[m[:, c], c]) for c in (0, 1, 4, 5))
+    err = float((np.abs(got - ref)[m] / np.maximum(1.0, np.abs(ref[m]))).max())
+    return {
+        "metric": "candidates/sec (8-feature path, 64-bin, 1k candidates)",
+        "value": n * steps / elapsed, "unit": "candidates/sec", "steps": steps,
+        "warmup": warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True,
+        "dtype": "u8->int64/f64", "data": "synthetic (SURVEY.md §8(d) recipe)",
+        "config": {"workload": f"config 1: {n} synthetic candidates, {lp}-bin profile + "
+                               f"{ld}-bin DM curve, 8 Lyon features; GPU pfe_lyon8_u8 "
+                               f"(resident rows) beside the CPU NumPy path"},
+        "avg_kernel_ms": kern_ms,
+        "gpu_from_host_arrays": {"value": n / host_s, "unit": "candidates/sec",
+                                 "ms_per_call": host_s * 1e3,
+                                 "note": "numpy in, numpy out: pinned staging + DMA each call"},
+        "cpu_baseline": {"value": n / cpu_s, "unit": "candidates/sec", "cores": 1,
+                         "kind": "port",
+                         "sample": f"the same {n} rows through oracle.lyon.lyon8 (per-candidate "
+                                   f"numpy mean/std + scipy skew/kurtosis), {cpu_s:.2f} s on 1 "
+                                   f"host core",
+                         **survey_validation("lyon8", n / cpu_s)},
+        "parity": {"mean_std_bit_exact": bool(exact), "max_rel_err": err},
+    }
+
+
 def bates_roofline(n, kern_ms, kern_max, kernel, ops=None):
     if ops is None:
         ops = load_ops_per_candidate()
@@ -805,6 +869,7 @@ def main():
             if not args.no_cpu_baseline:
                 r4["cpu_baseline"] = cpu_baseline_subband(256, 200)
             extra["config4"] = r4
+            extra["config1"] = run_config1(ctx)
             extra["config2_e2e"] = run_e2e(ctx, args, n, lp)
             torch.cuda.empty_cache()
             extra["lyon8_phcx"] = run_lyon8_phcx(ctx, args)
