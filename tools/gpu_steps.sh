@@ -5,7 +5,7 @@
 #
 # Every step runs under its own time limit, writes under gpurun_out/${TAG}_<step>*, and the
 # harness stops at the first failing step (no GPU work after a fault, abort or timeout).
-# TAG defaults to r05.  Steps:
+# TAG defaults to r06.  A/B of library builds: tools/ab.sh.  Steps:
 #   suite        pytest -m gpu (whole GPU suite)
 #   smoke        __graft_entry__.smoke()
 #   bench        bench.py --gpus 1 (the default bench line, all extras)
@@ -28,7 +28,7 @@ export TMPDIR=/tmp
 export PYTHONUNBUFFERED=1
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-T=${TAG:-r05}
+T=${TAG:-r06}
 O=gpurun_out
 
 fail() { echo "step $1 failed"; tail -40 "$2" 2>/dev/null; exit 1; }
