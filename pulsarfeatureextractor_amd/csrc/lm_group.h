@@ -143,15 +143,21 @@ __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
 }
 
 // qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%G, slot r/G)
-// rajjv[j] = 1 / a[j][j] of step j's Householder vector (0 for a zero column): the divisor
-// Q^T f divides by in glm_outer, so the contracted build takes it from here instead of a
-// second division
+// The per-column outputs are held DISTRIBUTED, element j in group lane j (j < N), not
+// replicated in every lane of the group: rdiag, acnorm and rajj = 1 / a[j][j] of step j's
+// Householder vector (0 for a zero column; the divisor Q^T f divides by in glm_outer, so the
+// contracted build takes it from here instead of a second division).  Element j is written
+// where the replicated loop had it (`if (gl == j)`), so the values are the same bits; the
+// registers are one pair per vector instead of N (the 8-parameter fit's register budget).
 template <int N, int MPL, int G = GLM_G>
-__device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
-                                        double (&acnorm)[N], double (&rajjv)[N]) {
+__device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double& rdiag,
+                                        double& acnorm, double& rajj) {
   PFE_LA_CONTRACT
   static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
   const int gl = glane<G>();
+  rdiag = 0.0;
+  acnorm = 0.0;
+  rajj = 0.0;
   // nrm: the partial column norms MINPACK keeps in rdiag while it factors (literal build), or
   // their squares (contracted build: the downdate r^2 - a^2, the pivot choice and the
   // norm-loss test need no square root; only the columns' own norms ajnorm and acnorm do)
@@ -169,8 +175,8 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
     gsum_from<N, G>(s, 0);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      acnorm[j] = SQ ? s[j] : sqrt(s[j]);  // squared in the contracted build (blm_simt roots it)
-      nrm[j] = acnorm[j];
+      nrm[j] = SQ ? s[j] : sqrt(s[j]);  // squared in the contracted build (blm_simt roots it)
+      if (gl == j) acnorm = nrm[j];
       wa[j] = nrm[j];
       ipvt[j] = j;
     }
@@ -218,7 +224,6 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       ajnorm = sqrt(pp);
       rinv = 1.0 / ajnorm;
     }
-    rajjv[j] = 0.0;
     if (ajnorm != 0.0) {
       if (gbcast<G>(a[0][j], j) < 0.0) {
         ajnorm = -ajnorm;
@@ -241,11 +246,11 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       }
       gsum_from<N, G>(d, j + 1);
       const double ajj = gbcast<G>(a[0][j], j);
-      const double rajj = 1.0 / ajj;
-      rajjv[j] = rajj;
+      const double rj = 1.0 / ajj;
+      if (gl == j) rajj = rj;
 #pragma unroll
       for (int c = j + 1; c < N; ++c) {
-        const double temp = la_quot(d[c], ajj, rajj);
+        const double temp = la_quot(d[c], ajj, rj);
 #pragma unroll
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
@@ -272,7 +277,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         }
       }
     }
-    rdiag[j] = -ajnorm;
+    if (gl == j) rdiag = -ajnorm;
   }
 }
 
@@ -373,26 +378,30 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   }
   nfev += N;
   int ipvt[N];
-  double rdiag[N], acn[N], rajjv[N];
+  double rdiag, acnl, rajj;  // group lane j < N holds element j (qrfac_g)
 #ifdef PFE_DUP_QR
   {
-    double a2[MPL][N], r2[N], c2[N], j2[N];
+    double a2[MPL][N], r2[1], c2, j2[1];
     int p2[N];
 #pragma unroll
     for (int k = 0; k < MPL; ++k)
 #pragma unroll
       for (int j = 0; j < N; ++j) a2[k][j] = fjac[k][j];
-    qrfac_g<N, MPL, G>(a2, p2, r2, c2, j2);
+    qrfac_g<N, MPL, G>(a2, p2, r2[0], c2, j2[0]);
     probe_keep(r2);
     probe_keep(j2);
   }
 #endif
-  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn, rajjv);
+  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acnl, rajj);
   // the contracted build leaves acn squared and the scaling (diag, and xnorm / delta of a
   // fresh fit) to the next SIMT phase, one fit per lane (blm_simt<.., true>)
   constexpr bool SQ = !LA_EXACT_QUOTIENTS;
-  double diag[N];
+  double diag[N], acn[N];
   double xnorm = 0.0, delta = 0.0;
+  if (!SQ) {  // the literal build's scaling update needs every column norm in every lane
+#pragma unroll
+    for (int j = 0; j < N; ++j) acn[j] = gbcast<G>(acnl, j);
+  }
   if (SQ) {
   } else if (iter == 1) {
     double wa3[N];
@@ -410,7 +419,6 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
 #pragma unroll
     for (int j = 0; j < N; ++j) diag[j] = S.diag[j][f];
   }
-  double qtf[N];
 #pragma unroll
   for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
   {
@@ -424,24 +432,27 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) p += fjac[k][j] * wa4[k];
       const double sum = gsum<G>(p);
-      const double temp = la_quot(-sum, ajj, rajjv[j]);
+      const double temp = la_quot(-sum, ajj, gbcast<G>(rajj, j));
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) wa4[k] = wa4[k] + fjac[k][j] * temp;
     }
-    if (gl == j) fjac[0][j] = rdiag[j];
-    qtf[j] = gbcast<G>(wa4[0], j);
+    if (gl == j) fjac[0][j] = rdiag;
   }
   }
+  // Q^T f: element j is row j of wa4 once column j is applied (later columns leave rows < j
+  // alone), i.e. slot 0 of group lane j -- each lane stores its own
 #pragma unroll
   for (int j = 0; j < N; ++j)
     if (gl <= j) S.r[tri_idx(0, j) + gl][f] = fjac[0][j];
+  if (gl < N) {
+    S.qtf[gl][f] = wa4[0];
+    S.acn[gl][f] = acnl;
+  }
   if (gl == 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       if (!SQ) S.diag[j][f] = fmax(diag[j], acn[j]);
-      S.qtf[j][f] = qtf[j];
-      S.acn[j][f] = acn[j];
       S.ipvt[j][f] = ipvt[j];
     }
     if (!SQ && iter == 1) {

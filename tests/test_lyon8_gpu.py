@@ -162,7 +162,10 @@ def test_phcx_ndm120_full_size_1m(engine):
         x = tp[s:s + (1 << 17)].to(torch.float64)
         mean = x.sum(dim=1) / 128.0
         std = torch.sqrt(((x - mean[:, None]) ** 2).sum(dim=1) / 128.0)
-        d = td[s:s + (1 << 17)].to(torch.float64).sum(dim=1) / float(ld)
+        # numpy's x.sum() / ld: an exact integer sum divided once, correctly rounded (on the
+        # host: torch divides by a scalar through its reciprocal)
+        d = torch.from_numpy(td[s:s + (1 << 17)].to(torch.float64).sum(dim=1).cpu().numpy()
+                             / float(ld)).to(out.device)
         o = out[s:s + (1 << 17)]
         assert torch.equal(o[:, 0], mean), f"profile mean, rows {s}.."
         assert torch.equal(o[:, 1], std), f"profile std, rows {s}.."
