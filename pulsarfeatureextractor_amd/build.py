@@ -53,11 +53,13 @@ def _needs(obj: str, deps: list[str]) -> bool:
 
 
 def build(verbose: bool = False, force: bool = False, variant: str = "",
-          defines: tuple[str, ...] = ()) -> str:
+          defines: tuple[str, ...] = (), csrc: str | None = None) -> str:
     """Compile every source and link lib/libpfe.so.  A non-empty ``variant`` builds an
     instrumented copy (lib/libpfe_<variant>.so, objects under lib/obj_<variant>/) with the
     extra -D ``defines`` (e.g. the LM phase-cycle profiler, -DPFE_LM_PROFILE); the product
-    library is never built with them."""
+    library is never built with them.  ``csrc``: another source tree for a variant (an A/B
+    against an earlier revision: tools/build_variant.py)."""
+    CSRC = csrc or globals()["CSRC"]
     builddir = BUILDDIR + (f"_{variant}" if variant else "")
     lib = os.path.join(LIBDIR, f"libpfe_{variant}.so") if variant else LIB
     extra = [f"-D{d}" for d in defines]

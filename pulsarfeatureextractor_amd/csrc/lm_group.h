@@ -566,18 +566,44 @@ __device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
   return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
 }
 
-// Hand the slots of `mask` to the groups, NG = 64/G per round; body(f) runs in the group
-// that owns slot f (lanes of other groups are masked off).
-template <int G, class Body>
-__device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body& body) {
+// Hand the slots of `mask` to the groups, NG = 64/G per round; body(f, fn) runs in the group
+// that owns slot f (lanes of other groups are masked off) with fn = prob.load(f), the slot's
+// residual functor (its data rows from global memory).
+//
+// PF: software-pipelined rounds -- the next round's functor loads are issued before this
+// round's body runs and consumed one round later, so their global-memory latency hides behind
+// a round of arithmetic instead of stalling the wave at the top of every round (at one or two
+// waves per SIMD nothing else hides it: SQ_WAIT_ANY 0.25-0.47 of the pooled kernels' cycles,
+// profiles/r05_bates22_sq_counters.json).  The loads, the bodies and their order are the
+// same, so are the results; it costs one functor's registers.
+#ifndef PFE_GLM_PF
+#define PFE_GLM_PF 1  // bit 0: T-phase rounds pipelined, bit 1: O-phase rounds
+#endif
+template <int G, bool PF, class Prob, class Body>
+__device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Prob& prob,
+                                           const Body& body) {
   const int lane = lane_id();
   const int cnt = __builtin_popcountll(mask);
   if ((mask >> lane) & 1ull) list[__builtin_popcountll(mask & ((1ull << lane) - 1ull))] = lane;
   blm_sync();
   const int g = lane / G;
-  for (int base = 0; base < cnt; base += 64 / G) {
-    const int idx = base + g;
-    if (idx < cnt) body(list[idx]);
+  constexpr int NG = 64 / G;
+  if constexpr (PF) {
+    using Fn = std::decay_t<decltype(prob.load(0))>;
+    Fn fn;
+    if (g < cnt) fn = prob.load(list[g]);
+    for (int base = 0; base < cnt; base += NG) {
+      const int idx = base + g, nidx = idx + NG;
+      Fn nfn;
+      if (nidx < cnt) nfn = prob.load(list[nidx]);
+      if (idx < cnt) body(list[idx], fn);
+      fn = nfn;
+    }
+  } else {
+    for (int base = 0; base < cnt; base += NG) {
+      const int idx = base + g;
+      if (idx < cnt) body(list[idx], prob.load(list[idx]));
+    }
   }
   blm_sync();
 }
@@ -632,8 +658,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // O-phase: fresh fits and accepted steps
     const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
     if (mo) {
-      glm_rounds<G>(mo, list, [&](int f) {
-        const auto fn = prob.load(f);
+      glm_rounds<G, (PFE_GLM_PF & 2) != 0>(mo, list, prob, [&](int f, const auto& fn) {
         glm_outer<N, MPL, FPW, G>(fn, f, S, ph[f] == PH_INIT, hand);
       });
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
@@ -660,8 +685,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // T-phase
     const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
     if (mt) {
-      glm_rounds<G>(mt, list, [&](int f) {
-        const auto fn = prob.load(f);
+      glm_rounds<G, (PFE_GLM_PF & 1) != 0>(mt, list, prob, [&](int f, const auto& fn) {
         const int nph = glm_trial<N, MPL, FPW, G>(fn, f, S, prob.maxfev(f), hand);
         if (glane<G>() == 0) ph[f] = nph;
       });

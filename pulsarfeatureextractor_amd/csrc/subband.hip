@@ -596,8 +596,20 @@ void k_subband_fast(SubArgs a) {
       if (off < total) {
         const int band = off / LSB;
         uint16_t* row = E + band * STRIDE + 16 * pos;
+#ifndef PFE_SB_NOSWZ
+        // a lane's 32 B go out as two 16-B stores; ds_write_b128 banks (dword mod 32) over 8
+        // contiguous lanes, and lanes pos and pos + 4 (32 B apart) would hit the same 4 banks
+        // if both stored their low half first: the upper four lanes of each eight store their
+        // halves in the other order (2-way conflicts -> none, same bytes)
+        const bool sw = (pos & 4) != 0;
+        reinterpret_cast<u32x4*>(row)[sw ? 1 : 0] =
+            sw ? (u32x4){pk[4], pk[5], pk[6], pk[7]} : (u32x4){pk[0], pk[1], pk[2], pk[3]};
+        reinterpret_cast<u32x4*>(row)[sw ? 0 : 1] =
+            sw ? (u32x4){pk[0], pk[1], pk[2], pk[3]} : (u32x4){pk[4], pk[5], pk[6], pk[7]};
+#else
         reinterpret_cast<u32x4*>(row)[0] = (u32x4){pk[0], pk[1], pk[2], pk[3]};
         reinterpret_cast<u32x4*>(row)[1] = (u32x4){pk[4], pk[5], pk[6], pk[7]};
+#endif
         if (pos == SEG - 1) {
           row[16] = (uint16_t)(excl + tot);  // E[band][LSB] = T (in the zeroed tail)
           bstat[3 * band + 0] = (int)(excl + tot);
@@ -648,7 +660,16 @@ void k_subband_fast(SubArgs a) {
   // dwords); the steps run in chunks of 4 (skipped past the last window), and a window
   // j >= nw of the last chunk reads E[j + wb] from the zero tail of its row (indices up to
   // lsb + 22), so its saturated difference is 0: no masks
+#ifndef PFE_SB_NOSWZ
+  // u16 reads bank on (dword mod 32) per 32-lane half: with a row pitch of 4 x odd dwords,
+  // bands bi and bi + 8 start on the same bank, so the half's two quarter lanes of each band
+  // would collide 2-way; bands 8-15 take the quarters in the order 2, 3, 0, 1, which puts the
+  // 32 lanes of a half on 32 distinct dwords (the four quarter lanes of a band still cover
+  // every window once; sums and maxima are order-free integers: the same results)
+  const int bi = lane & 15, qtr = (lane >> 4) ^ ((bi >> 3) << 1);
+#else
   const int bi = lane & 15, qtr = lane >> 4;
+#endif
   const int U = 2 * ((nw + 7) >> 3);
   constexpr int NCH = (LSB / 4 + 3) / 4;
   for (int blk = 0; blk < nsub; blk += SB_NB) {
