@@ -769,6 +769,11 @@ __device__ __forceinline__ double wave_sum_tri_f64(double v) {
 
 constexpr int DM_S = 132;                     // LDS leaf stride
 constexpr int DM_IMG_BYTES = 64 * DM_S;       // one chunk image per wave (8448 B)
+// two one-chunk tri rows per wave (G == 32 of lyon8_u8_dm): a lane's slot holds a block's
+// 128-byte leaf (even lane) or its 64- and 72-byte leaves back to back (odd lane, 136 B); the
+// stride 140 = 4 x 35 (odd dwords) keeps a ds_read_u8 group's 32 lanes on 32 banks
+constexpr int DM_S_T = 140;
+constexpr int DM_IMG_T = 64 * DM_S_T;         // 8960 B
 
 // 64-lane sum of a 32-bit value: DPP within rows, then the four row sums through the
 // permlane swaps.  Exact; every lane ends with the total.
@@ -917,6 +922,62 @@ __device__ __forceinline__ double wave_sum_tri_split_f64(double v) {
   return row_total_f64(v);
 }
 
+// Two one-chunk tri rows per wave (G == 32 of lyon8_u8_dm; nDM = 33): each half-wave holds
+// a row's 16 blocks, block b in lanes 2b (its 128-byte leaf) and 2b + 1 (the 64- and 72-byte
+// leaves, 136 bytes in a row of the image).  One loop of 17 words of 8 bytes, all 8 chains per
+// lane: the even lane adds its 16 words (the 17th adds +0.0, which leaves a non-negative sum's
+// bits alone); the odd lane adds the 64-byte leaf's 8 words, parks its chains at word 8 and
+// restarts them for the 72-byte leaf's 9.  Returns the big leaf's tree, or L64 + L72 -- so the
+// half-wave butterfly's first step (lane ^ 1) forms numpy's block L0 + (L64 + L72) and its
+// remaining steps the perfect tree over the 16 blocks (half_sum_f64).
+template <bool FPM>
+__device__ __forceinline__ double dm_leaf_tri_pair(const uint8_t* img, int lane, double nm,
+                                                   double sc, const uint32_t (&z)[8], double& a3,
+                                                   double& a4) {
+  typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8;
+  const bool odd = (lane & 1) != 0;
+  lds_u8* vb = (lds_u8*)(img + lane * DM_S_T);
+  double r[8], sv[8];
+  double c3[2] = {0.0, 0.0}, c4[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 17; ++k) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = vb[8 * k + j];
+    if (k == 8) {  // the odd lane: the 64-byte leaf is done, its chains restart
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sv[j] = r[j];
+        r[j] = odd ? 0.0 : r[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double X = __builtin_bit_cast(double, ((uint64_t)z[j] << 32) | x[j]);
+      const double d = __builtin_fma(sc, X, nm);
+      double sq = d * d;
+      if (k == 16) sq = odd ? sq : 0.0;
+      r[j] = k == 0 ? sq : r[j] + sq;
+      if constexpr (FPM) {
+        c3[j & 1] = __builtin_fma(sq, d, c3[j & 1]);
+        c4[j & 1] = __builtin_fma(sq, sq, c4[j & 1]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(r[j]));
+    if (k >= 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(sv[j]));
+    }
+    if constexpr (FPM) asm volatile("" : "+v"(c3[0]), "+v"(c3[1]), "+v"(c4[0]), "+v"(c4[1]));
+  }
+  a3 = c3[0] + c3[1];
+  a4 = c4[0] + c4[1];
+  const double tr = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  const double ts = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
+  return odd ? ts + tr : tr;
+}
+
 // Sums over each 32-lane half of the wave (two rows per wave, G == 16 of lyon8_u8_dm): the
 // in-row DPP steps of wave_sum_* and one exchange with lane ^ 16 -- for 32 leaves numpy's
 // (tree of 0..15) + (tree of 16..31), for fewer the rows past them add +0.0
@@ -944,6 +1005,7 @@ __device__ __forceinline__ double half_sum_f64(double v) {
 template <int NCH, int NPMAX>
 __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], int ch, int lane,
                                          uint32_t full_base, const uint16_t* stab) {
+  constexpr int NPL = NPMAX - 8 * (NCH - 1);  // pieces of the last chunk (9: tri pairs)
   typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;
   if (ch < NCH - 1) {
     // (volatile: single ds_write_b32 with 16-bit immediate offsets from one base register,
@@ -959,7 +1021,7 @@ __device__ __forceinline__ void dm_stage(uint8_t* img, const u32x4 (&q)[NPMAX], 
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NPL; ++j) {
       const u32x4 v = q[8 * ch + j];
       const uint32_t a0 = stab[(2 * j) * 64 + lane], a1 = stab[(2 * j + 1) * 64 + lane];
       if (a0 != 0xFFFFu) {
@@ -992,29 +1054,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 2 ? 
 void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __restrict__ dm,
                  int64_t ds, int64_t n, double* __restrict__ out, DmShape sh) {
   static_assert(NCH >= 1 && NCH <= 4, "DataBlocks of up to 4 numpy chunks (nDM <= 256)");
-  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 3 || G == 16,
-                "lanes per leaf (3: the tri form split; 16: two one-chunk rows per wave)");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 3 || G == 16 || G == 32,
+                "lanes per leaf (3: the tri form split; 16: two one-chunk rows per wave; 32: two "
+                "one-chunk tri rows per wave)");
   // G == 16: one-chunk rows of <= 32 leaves two at a time, row c in lanes 0-31 and row c + 1
-  // in lanes 32-63 (one leaf per lane, every per-row step shared by two rows)
-  constexpr bool PAIR = G == 16;
+  // in lanes 32-63 (one leaf per lane, every per-row step shared by two rows); G == 32 the
+  // same for one-chunk tri rows (nDM = 33, 4224 bytes: nine 16-byte pieces per lane, two lanes
+  // per 264-byte block, dm_leaf_tri_pair)
+  constexpr bool PAIRT = G == 32;
+  constexpr bool PAIR = G == 16 || PAIRT;
   static_assert(!PAIR || (NCH == 1 && FPM), "pairs: one-chunk rows, fp64 moments");
-  constexpr int NPMAX = 8 * NCH;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[4][DM_IMG_BYTES];
-  __shared__ uint16_t stab[16 * 64];  // last chunk: LDS address of half h of piece j, lane l
+  constexpr int NPMAX = PAIRT ? 9 : 8 * NCH;
+  constexpr int NPL = NPMAX - 8 * (NCH - 1);  // 16-byte pieces of the last chunk per lane
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][PAIRT ? DM_IMG_T : DM_IMG_BYTES];
+  __shared__ uint16_t stab[2 * NPL * 64];  // last chunk: LDS address of half h of piece j, lane l
   const int lane = threadIdx.x & 63;
   uint8_t* img = lds[threadIdx.x >> 6];
   // the block's staging table (row-invariant): half h of lane l's piece j holds chunk bytes
   // o = 16 l + 1024 j + 8 h, i.e. bytes o - start(L) of leaf L (pairs: o = 16 (l % 32) +
-  // 512 j + 8 h of the half's row, its leaf L at slot 32 (l / 32) + L)
-  for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {
+  // 512 j + 8 h of the half's row, its leaf L at slot 32 (l / 32) + L; tri pairs: block
+  // b = o / 264 at slots 2b (bytes 0-127) and 2b + 1 (bytes 128-263) of stride DM_S_T)
+  for (int e = threadIdx.x; e < 2 * NPL * 64; e += blockDim.x) {
     const int jh = e >> 6, l = e & 63;
     const int o = PAIR ? 16 * (l & 31) + 512 * (jh >> 1) + 8 * (jh & 1)
                        : 16 * l + 1024 * (jh >> 1) + 8 * (jh & 1);
     uint16_t a = 0xFFFFu;
     if (o < sh.len_last) {
-      int L = 0;
-      while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
-      a = (uint16_t)(((PAIR ? 32 * (l >> 5) : 0) + dm_leaf_lane(sh, L)) * DM_S + (o - sh.start[L]));
+      if constexpr (PAIRT) {
+        const int b = o / 264, w = o % 264;
+        a = (uint16_t)((32 * (l >> 5) + 2 * b + (w < 128 ? 0 : 1)) * DM_S_T + (w < 128 ? w : w - 128));
+      } else {
+        int L = 0;
+        while (L + 1 < sh.leaves_last && sh.start[L + 1] <= o) ++L;
+        a = (uint16_t)(((PAIR ? 32 * (l >> 5) : 0) + dm_leaf_lane(sh, L)) * DM_S + (o - sh.start[L]));
+      }
     }
     stab[e] = a;
   }
@@ -1030,7 +1103,7 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
   for (int k = 0; k < NPMAX; ++k) zpad += 16 * (lane + 64 * k) >= sh.ld ? 16 : 0;
   const uint32_t full_base = 16u * lane + 4u * (lane >> 3);  // leaf lane/8, offset 16*(lane%8)
   // this lane's leaf of the last chunk (-1: none) and its 8-byte words
-  const int leaf_last = G == 3 ? 0  // every lane of the split tri form holds a part
+  const int leaf_last = (G == 3 || PAIRT) ? 0  // every lane of the split / paired tri form holds a part
                       : PAIR ? ((lane & 31) < sh.leaves_last ? (lane & 31) : -1)
                       : sh.tri ? ((lane & 3) < 3 ? 3 * (lane >> 2) + (lane & 3) : -1)
                                : (lane / G < sh.leaves_last ? lane / G : -1);
@@ -1128,7 +1201,9 @@ void lyon8_u8_dm(const uint8_t* __restrict__ prof, int64_t ps, const uint8_t* __
         wave_lds_sync();
         double l3, l4;
         double leaf;
-        if (G == 3 && ch == NCH - 1)  // the tri form, its big leaf split by chains
+        if (PAIRT)  // two tri rows per wave, two lanes per block
+          leaf = dm_leaf_tri_pair<FPM>(img, lane, nm, sc, z, l3, l4);
+        else if (G == 3 && ch == NCH - 1)  // the tri form, its big leaf split by chains
           leaf = dm_leaf_tri<FPM>(img, lane, nm, sc, z, l3, l4);
         else if (G == 2 || G == 4 || G == 8) {  // the last chunk's leaf lane / G, chains of this lane
           if (ch == NCH - 1)
@@ -1419,6 +1494,8 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     // lanes per leaf of the last chunk: a last chunk of <= 32 leaves is split by chains
     // (PFE_OPT_LYON8_DM_SPLIT = 0 keeps one lane per leaf)
     const int G = !o.lyon8_dm_split ? 1
+                  // one-chunk tri rows (nDM = 33) two per wave, as the 17-32-leaf rows below
+                  : (dsh.tri && dnch == 1 && o.lyon8_dm_split == 1) ? 32
                   : dsh.tri ? 3  // the tri form's big leaf split by chains
                   // two one-chunk rows per wave where a chain split would only halve the
                   // leaves' work (32 leaves); at <= 16 the 4- and 8-lane splits are faster
@@ -1433,6 +1510,7 @@ hipError_t launch_lyon8_u8(const uint8_t* prof, int64_t ps, int lp, const uint8_
     case 2: launch_dm_kernel<C, true, 2>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 3: launch_dm_kernel<C, true, 3>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     case 16: if constexpr (C == 1) launch_dm_kernel<1, true, 16>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
+    case 32: if constexpr (C == 1) launch_dm_kernel<1, true, 32>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
     default: launch_dm_kernel<C, true, 1>(prof, ps, dm, ds, n, out, dsh, st, cap); break; \
   }
       switch (dnch) {

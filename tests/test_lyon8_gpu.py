@@ -277,13 +277,16 @@ def test_long_dm_rows_golden_dmplane(engine):
 
 @pytest.mark.parametrize("lp,ld", [(128, 3840), (128, 9216), (128, 20480), (64, 1024),
                                    (128, 8448), (256, 10240), (128, 2048), (128, 24704),
-                                   (128, 4224), (128, 12416), (64, 28800)])
+                                   (128, 4224), (128, 12416), (64, 28800), (64, 4224),
+                                   (256, 4224)])
 def test_long_dm_rows_split_last_chunk(engine, lp, ld):
     """Last numpy chunks of <= 32 leaves (nDM = 30, 72, 160, 8, 66, 80, 16, 193: 32, 8, 32, 8,
     2, 16, 16 and 1 leaves) summed by 2, 4 or 8 lanes per leaf, each with some of the leaf's 8
     chains, the tri form (nDM = 33, 97, 225) with its 128-byte leaves split over the quad's
     idle lane, and one-chunk rows of <= 32 leaves (nDM = 30, 8, 16) two per wave (round 5,
-    PFE_OPT_LYON8_DM_SPLIT 1; 2 = the chain splits only): mean and std bit-identical to one
+    PFE_OPT_LYON8_DM_SPLIT 1; 2 = the chain splits only), and since round 6 the one-chunk tri
+    rows (nDM = 33, 64/128/256-byte profiles) two per wave as well, two lanes per 264-byte
+    block (G = 32; option 2 keeps the quad split): mean and std bit-identical to one
     lane per leaf and bit-exact against the oracle; skew / kurt (their d^3 / d^4 sums are
     grouped by lane, in any order) within 1e-12 of one lane per leaf.  An odd row count and a
     one-block grid (several 64-row batches per wave, a lone last row) cover the pairs' edges."""

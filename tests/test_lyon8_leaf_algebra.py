@@ -51,3 +51,54 @@ def test_exact_leaf_std_matches_numpy(n):
         rows.append(rng.integers(lo, lo + int(rng.integers(1, 56)), n).astype(np.uint8))
     for r in rows:
         assert std_exact_leaves(r) == np.std(r)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_paired_tri_rows_layout_matches_numpy(seed):
+    """lyon8_u8_dm<1, true, 32> (two one-chunk tri rows per wave, nDM = 33): the staging
+    table's image layout (block b's 128-byte leaf in slot 2b, its 64- and 72-byte leaves back
+    to back in slot 2b + 1, stride DM_S_T = 140), dm_leaf_tri_pair's 17-word chain loop with
+    the odd lane's restart at word 8, and half_sum_f64's butterfly (lane ^ 1, ^ 2, half-row and
+    row mirrors, ^ 16) give numpy's sum of squared deviations of the 4224-byte row bit for bit
+    (the kernel works in a power-of-two scaled domain, which is exact; adversarial rows too)."""
+    S = 140
+    rng = np.random.default_rng(100 + seed)
+    x = rng.integers(0, 256, 4224).astype(np.uint8)
+    if seed == 1:
+        x[:] = 255
+        x[::7] = 0
+    if seed == 2:
+        x = np.sort(x)
+    mean = x.astype(np.float64).sum() / 4224
+    ref = np.sum((x.astype(np.float64) - mean) ** 2)
+    img = np.zeros(32 * S, np.uint8)
+    for ln in range(32):
+        for j in range(9):
+            for h in range(2):
+                o = 16 * ln + 512 * j + 8 * h
+                if o < 4224:
+                    b, w = divmod(o, 264)
+                    a = (2 * b + (w >= 128)) * S + (w if w < 128 else w - 128)
+                    img[a:a + 8] = x[o:o + 8]
+    vals = []
+    for ln in range(32):
+        odd = ln & 1
+        vb = img[ln * S:ln * S + 136].astype(np.float64)
+        r, sv = [0.0] * 8, [0.0] * 8
+        for k in range(17):
+            if k == 8:
+                sv = list(r)
+                if odd:
+                    r = [0.0] * 8
+            for j in range(8):
+                d = vb[8 * k + j] - mean if 8 * k + j < 136 else 0.0
+                sq = d * d if (k < 16 or odd) else 0.0
+                r[j] = sq if k == 0 else r[j] + sq
+        tr = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        ts = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]))
+        vals.append(ts + tr if odd else tr)
+    v = np.array(vals)
+    for perm in (lambda i: i ^ 1, lambda i: i ^ 2, lambda i: (i & ~7) | (7 - (i & 7)),
+                 lambda i: (i & ~15) | (15 - (i & 15)), lambda i: i ^ 16):
+        v = np.array([v[i] + v[perm(i)] for i in range(32)])
+    assert (v == ref).all()

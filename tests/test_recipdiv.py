@@ -30,6 +30,10 @@ int main(int argc, char** argv) {
     double b = mk(-500, 499, mode == 1);
     double a = mk(-900, 400, mode == 2);
     if (mode == 3) { b = mk(-3, 3, 0); a = mk(-2, 8, 0); }   /* the fits' usual range */
+    if (argc > 2) {  /* the DM model's constant divisor F3 = 1374^3 (div_f3) */
+      b = 2593941624.0;
+      a = (i & 1) ? mk(-900, 900, 0) : mk(20, 40, 0);
+    }
     volatile double y = 1.0 / b;
     volatile double q = a * y;
     volatile double r = fma(-q, b, a);
@@ -54,6 +58,11 @@ def test_shared_divisor_quotient_is_correctly_rounded():
         open(c, "w").write(SRC.replace("#include <string.h>", "#include <string.h>\n#include <stdlib.h>"))
         subprocess.run(["gcc", "-O2", "-ffp-contract=off", c, "-o", exe, "-lm"], check=True)
         out = subprocess.run([exe, "4000000"], capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stdout
+        n, bad = map(int, out.stdout.split()[-2:])
+        assert n == 4000000 and bad == 0
+        # div_f3 of the DM-curve model (bates_sine_dm_sub.hip): b = F3, |a| in [2^-900, 2^900]
+        out = subprocess.run([exe, "4000000", "f3"], capture_output=True, text=True, timeout=120)
         assert out.returncode == 0, out.stdout
         n, bad = map(int, out.stdout.split()[-2:])
         assert n == 4000000 and bad == 0
