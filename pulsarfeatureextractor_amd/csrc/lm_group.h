@@ -579,6 +579,31 @@ __device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
 #ifndef PFE_GLM_PF
 #define PFE_GLM_PF 1  // bit 0: T-phase rounds pipelined, bit 1: O-phase rounds
 #endif
+// per kernel (glm_engine's PF argument; each defaults to PFE_GLM_PF)
+#ifndef PFE_PF_GHIST
+#define PFE_PF_GHIST PFE_GLM_PF
+#endif
+#ifndef PFE_PF_GFIX
+#define PFE_PF_GFIX PFE_GLM_PF
+#endif
+#ifndef PFE_PF_GT1
+#define PFE_PF_GT1 PFE_GLM_PF
+#endif
+#ifndef PFE_PF_GDG
+#define PFE_PF_GDG PFE_GLM_PF
+#endif
+#ifndef PFE_PF_GDG8
+#define PFE_PF_GDG8 PFE_GLM_PF
+#endif
+#ifndef PFE_PF_SINE
+#define PFE_PF_SINE PFE_GLM_PF
+#endif
+#ifndef PFE_PF_DM
+#define PFE_PF_DM PFE_GLM_PF
+#endif
+#ifndef PFE_PF_PFDDM
+#define PFE_PF_PFDDM PFE_GLM_PF
+#endif
 template <int G, bool PF, class Prob, class Body>
 __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Prob& prob,
                                            const Body& body) {
@@ -617,7 +642,7 @@ __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Prob&
 // ph / list: LDS int[FPW] each.  hand_region: hand-over scratch of FPW x hand_k x G doubles
 // per wave (block), or nullptr.  G: lanes per group (16 or 32; Prob::load lays the rows out
 // for the same G).
-template <int N, int MPL, int FPW, int G = GLM_G, class Prob>
+template <int N, int MPL, int FPW, int G = GLM_G, int PF = PFE_GLM_PF, class Prob>
 __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list,
                                            double* hand_region = nullptr, int hand_k = 0) {
   static_assert(FPW <= 64, "one slot per lane in the SIMT phase");
@@ -658,7 +683,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // O-phase: fresh fits and accepted steps
     const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
     if (mo) {
-      glm_rounds<G, (PFE_GLM_PF & 2) != 0>(mo, list, prob, [&](int f, const auto& fn) {
+      glm_rounds<G, (PF & 2) != 0>(mo, list, prob, [&](int f, const auto& fn) {
         glm_outer<N, MPL, FPW, G>(fn, f, S, ph[f] == PH_INIT, hand);
       });
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
@@ -685,7 +710,7 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // T-phase
     const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
     if (mt) {
-      glm_rounds<G, (PFE_GLM_PF & 1) != 0>(mt, list, prob, [&](int f, const auto& fn) {
+      glm_rounds<G, (PF & 1) != 0>(mt, list, prob, [&](int f, const auto& fn) {
         const int nph = glm_trial<N, MPL, FPW, G>(fn, f, S, prob.maxfev(f), hand);
         if (glane<G>() == 0) ph[f] = nph;
       });

@@ -60,6 +60,10 @@ def main():
                          "opened, inflated and parsed)")
     ap.add_argument("--depth", default="2",
                     help="GPU pipeline depths to time, comma-separated (DataProcessor gpu_depth)")
+    ap.add_argument("--gpus", default="1",
+                    help="stream mode: shard counts to time, comma-separated (DataProcessor "
+                         "gpus=N: N spawned workers, each on GPU r %% visible GPUs, the host "
+                         "threads split between them)")
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     have = sorted(f for f in os.listdir(args.dir) if f.endswith(".phcx.gz"))
@@ -100,12 +104,14 @@ def main():
         res["reader_parse_pack_files_per_s"] = nfiles / (time.perf_counter() - t0)
         eng = get_engine(0)
         texts = {}
-        for depth in (int(v) for v in args.depth.split(",")):
+        runs = [(int(d), 1) for d in args.depth.split(",")]
+        runs += [(int(args.depth.split(",")[-1]), int(g)) for g in args.gpus.split(",") if int(g) > 1]
+        for depth, g in runs:
             for kind in ("scores", "dmprof"):
                 out = os.path.join(tempfile.mkdtemp(), "scores.csv")
                 dp = processor.DataProcessor(engine=eng, workers=args.workers,
                                              log=lambda *a: None, batch=args.batch,
-                                             gpu_depth=depth, ramp=bool(args.ramp))
+                                             gpu_depth=depth, ramp=bool(args.ramp), gpus=g)
                 t0 = time.perf_counter()
                 if kind == "scores":
                     dp.processPHCXCollectively(args.dir, False, out, False, False, False)
@@ -115,7 +121,8 @@ def main():
                 with open(out) as f:
                     text = f.read()
                 same = texts.setdefault(kind, text) == text
-                res[f"{kind}_depth{depth}"] = {"wall_s": wall, "files_per_s": nfiles / wall,
+                res[f"{kind}_depth{depth}" + (f"_gpus{g}" if g > 1 else "")] = {
+                                               "wall_s": wall, "files_per_s": nfiles / wall,
                                                "lines": text.count("\n"),
                                                "text_identical_to_first_depth": same,
                                                "metrics": dp.metrics}
