@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(64, 2) void k_ghistg(BatesArgs a) {
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   GhistProb<P, F, FPW> prob{a, T, HS, cnt, hist, stage, a.gslots};
-  glm_engine<3, 4, FPW, GLM_G, PFE_PF_GHIST>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  glm_engine<3, 4, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 template <int P, bool F, int FPW>
@@ -1135,7 +1135,7 @@ __global__ __launch_bounds__(64, 2) void k_gfixg(BatesArgs a) {
   blm_sync();
   double* cnt = a.wscr + (size_t)blockIdx.x * gdg_wave_scratch_doubles(a.lp);
   GfixProb<P, F, FPW> prob{a, T, cnt, hist, a.gslots};
-  glm_engine<2, 4, FPW, GLM_G, PFE_PF_GFIX>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  glm_engine<2, 4, FPW>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2077,7 +2077,7 @@ __global__ __launch_bounds__(64, PFE_GT1G_WPE) void k_gt1g(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   Gt1Prob<P, FPW, G> prob{a, T, a.gslots * FPW / GLM_FPW};
-  glm_engine<4, 64 * P / G, FPW, G, PFE_PF_GT1>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the 8 peel passes ----------------------------------------------------------
@@ -2201,7 +2201,7 @@ __global__ __launch_bounds__(64, PFE_GDGG_WPE) void k_gdgg(BatesArgs a) {
   double* yv = xs + (size_t)FPW * 64 * P;
   constexpr int G = glm_group_lanes(64 * P);
   PeelProb<P, FPW, G> prob{a, T, xs, yv, ys, cx, a.gslots * FPW / GLM_FPW};
-  glm_engine<4, 64 * P / G, FPW, G, PFE_PF_GDG>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  glm_engine<4, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 // ---- s10, s11: the final 8-parameter fit ----------------------------------------------
@@ -2271,7 +2271,7 @@ __global__ __launch_bounds__(64, PFE_GDG8_WPE) void k_gdg8g(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   Gdg8Prob<P, FPW, G> prob{a, T, a.gslots * GDG8_FPW / GLM_FPW};
-  glm_engine<8, 64 * P / G, FPW, G, PFE_PF_GDG8>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
+  glm_engine<8, 64 * P / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_GAUSS], HAND_K_GAUSS);
 }
 
 static inline dim3 gw(int64_t n) { return grid_for_candidates(n); }

@@ -418,7 +418,7 @@ __global__ __launch_bounds__(64, 3) void k_sineg(BatesArgs a) {
   blm_sync();
   constexpr int G = glm_group_lanes(64 * MPL);
   SineProb<MPL, F, FPW, G> prob{a, T, stage, a.gslots};
-  glm_engine<2, 64 * MPL / G, FPW, G, PFE_PF_SINE>(prob, S, T.ph, T.list, a.hand[HAND_SINE], HAND_K_SINE);
+  glm_engine<2, 64 * MPL / G, FPW, G>(prob, S, T.ph, T.list, a.hand[HAND_SINE], HAND_K_SINE);
 }
 
 // ======================================================================================
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(64, 3) void k_dmfitg(BatesArgs a) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   DMProb<MPL, FPW> prob{a, T, a.gslots};
-  glm_engine<3, 4 * MPL, FPW, GLM_G, PFE_PF_DM>(prob, S, T.ph, T.list, a.hand[HAND_DM], HAND_K_DM);
+  glm_engine<3, 4 * MPL, FPW>(prob, S, T.ph, T.list, a.hand[HAND_DM], HAND_K_DM);
 }
 
 // ---- launchers -----------------------------------------------------------------------

@@ -143,21 +143,15 @@ __device__ __forceinline__ double enorm_g(const double (&f)[MPL]) {
 }
 
 // qrfac (pivot = true) on the group-distributed m x N matrix a (row r: lane r%G, slot r/G)
-// The per-column outputs are held DISTRIBUTED, element j in group lane j (j < N), not
-// replicated in every lane of the group: rdiag, acnorm and rajj = 1 / a[j][j] of step j's
-// Householder vector (0 for a zero column; the divisor Q^T f divides by in glm_outer, so the
-// contracted build takes it from here instead of a second division).  Element j is written
-// where the replicated loop had it (`if (gl == j)`), so the values are the same bits; the
-// registers are one pair per vector instead of N (the 8-parameter fit's register budget).
+// rajjv[j] = 1 / a[j][j] of step j's Householder vector (0 for a zero column): the divisor
+// Q^T f divides by in glm_outer, so the contracted build takes it from here instead of a
+// second division
 template <int N, int MPL, int G = GLM_G>
-__device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double& rdiag,
-                                        double& acnorm, double& rajj) {
+__device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], double (&rdiag)[N],
+                                        double (&acnorm)[N], double (&rajjv)[N]) {
   PFE_LA_CONTRACT
   static_assert(N <= 16, "diagonal rows must sit in slot 0 of the group's first DPP row");
   const int gl = glane<G>();
-  rdiag = 0.0;
-  acnorm = 0.0;
-  rajj = 0.0;
   // nrm: the partial column norms MINPACK keeps in rdiag while it factors (literal build), or
   // their squares (contracted build: the downdate r^2 - a^2, the pivot choice and the
   // norm-loss test need no square root; only the columns' own norms ajnorm and acnorm do)
@@ -175,8 +169,8 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
     gsum_from<N, G>(s, 0);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      nrm[j] = SQ ? s[j] : sqrt(s[j]);  // squared in the contracted build (blm_simt roots it)
-      if (gl == j) acnorm = nrm[j];
+      acnorm[j] = SQ ? s[j] : sqrt(s[j]);  // squared in the contracted build (blm_simt roots it)
+      nrm[j] = acnorm[j];
       wa[j] = nrm[j];
       ipvt[j] = j;
     }
@@ -224,6 +218,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       ajnorm = sqrt(pp);
       rinv = 1.0 / ajnorm;
     }
+    rajjv[j] = 0.0;
     if (ajnorm != 0.0) {
       if (gbcast<G>(a[0][j], j) < 0.0) {
         ajnorm = -ajnorm;
@@ -246,11 +241,11 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
       }
       gsum_from<N, G>(d, j + 1);
       const double ajj = gbcast<G>(a[0][j], j);
-      const double rj = 1.0 / ajj;
-      if (gl == j) rajj = rj;
+      const double rajj = 1.0 / ajj;
+      rajjv[j] = rajj;
 #pragma unroll
       for (int c = j + 1; c < N; ++c) {
-        const double temp = la_quot(d[c], ajj, rj);
+        const double temp = la_quot(d[c], ajj, rajj);
 #pragma unroll
         for (int k = 0; k < MPL; ++k)
           if (row_ge(gl, k, j)) a[k][c] = a[k][c] - temp * a[k][j];
@@ -277,7 +272,7 @@ __device__ __forceinline__ void qrfac_g(double (&a)[MPL][N], int (&ipvt)[N], dou
         }
       }
     }
-    if (gl == j) rdiag = -ajnorm;
+    rdiag[j] = -ajnorm;
   }
 }
 
@@ -378,30 +373,26 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
   }
   nfev += N;
   int ipvt[N];
-  double rdiag, acnl, rajj;  // group lane j < N holds element j (qrfac_g)
+  double rdiag[N], acn[N], rajjv[N];
 #ifdef PFE_DUP_QR
   {
-    double a2[MPL][N], r2[1], c2, j2[1];
+    double a2[MPL][N], r2[N], c2[N], j2[N];
     int p2[N];
 #pragma unroll
     for (int k = 0; k < MPL; ++k)
 #pragma unroll
       for (int j = 0; j < N; ++j) a2[k][j] = fjac[k][j];
-    qrfac_g<N, MPL, G>(a2, p2, r2[0], c2, j2[0]);
+    qrfac_g<N, MPL, G>(a2, p2, r2, c2, j2);
     probe_keep(r2);
     probe_keep(j2);
   }
 #endif
-  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acnl, rajj);
+  qrfac_g<N, MPL, G>(fjac, ipvt, rdiag, acn, rajjv);
   // the contracted build leaves acn squared and the scaling (diag, and xnorm / delta of a
   // fresh fit) to the next SIMT phase, one fit per lane (blm_simt<.., true>)
   constexpr bool SQ = !LA_EXACT_QUOTIENTS;
-  double diag[N], acn[N];
+  double diag[N];
   double xnorm = 0.0, delta = 0.0;
-  if (!SQ) {  // the literal build's scaling update needs every column norm in every lane
-#pragma unroll
-    for (int j = 0; j < N; ++j) acn[j] = gbcast<G>(acnl, j);
-  }
   if (SQ) {
   } else if (iter == 1) {
     double wa3[N];
@@ -419,6 +410,7 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
 #pragma unroll
     for (int j = 0; j < N; ++j) diag[j] = S.diag[j][f];
   }
+  double qtf[N];
 #pragma unroll
   for (int k = 0; k < MPL; ++k) wa4[k] = fvec[k];
   {
@@ -432,27 +424,24 @@ __device__ __forceinline__ void glm_outer(const Fn& fcn, int f, BlmState<N, FPW>
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) p += fjac[k][j] * wa4[k];
       const double sum = gsum<G>(p);
-      const double temp = la_quot(-sum, ajj, gbcast<G>(rajj, j));
+      const double temp = la_quot(-sum, ajj, rajjv[j]);
 #pragma unroll
       for (int k = 0; k < MPL; ++k)
         if (row_ge(gl, k, j)) wa4[k] = wa4[k] + fjac[k][j] * temp;
     }
-    if (gl == j) fjac[0][j] = rdiag;
+    if (gl == j) fjac[0][j] = rdiag[j];
+    qtf[j] = gbcast<G>(wa4[0], j);
   }
   }
-  // Q^T f: element j is row j of wa4 once column j is applied (later columns leave rows < j
-  // alone), i.e. slot 0 of group lane j -- each lane stores its own
 #pragma unroll
   for (int j = 0; j < N; ++j)
     if (gl <= j) S.r[tri_idx(0, j) + gl][f] = fjac[0][j];
-  if (gl < N) {
-    S.qtf[gl][f] = wa4[0];
-    S.acn[gl][f] = acnl;
-  }
   if (gl == 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       if (!SQ) S.diag[j][f] = fmax(diag[j], acn[j]);
+      S.qtf[j][f] = qtf[j];
+      S.acn[j][f] = acn[j];
       S.ipvt[j][f] = ipvt[j];
     }
     if (!SQ && iter == 1) {
@@ -566,69 +555,18 @@ __device__ __forceinline__ int64_t queue_next(unsigned* ctr) {
   return (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)c);
 }
 
-// Hand the slots of `mask` to the groups, NG = 64/G per round; body(f, fn) runs in the group
-// that owns slot f (lanes of other groups are masked off) with fn = prob.load(f), the slot's
-// residual functor (its data rows from global memory).
-//
-// PF: software-pipelined rounds -- the next round's functor loads are issued before this
-// round's body runs and consumed one round later, so their global-memory latency hides behind
-// a round of arithmetic instead of stalling the wave at the top of every round (at one or two
-// waves per SIMD nothing else hides it: SQ_WAIT_ANY 0.25-0.47 of the pooled kernels' cycles,
-// profiles/r05_bates22_sq_counters.json).  The loads, the bodies and their order are the
-// same, so are the results; it costs one functor's registers.
-#ifndef PFE_GLM_PF
-#define PFE_GLM_PF 1  // bit 0: T-phase rounds pipelined, bit 1: O-phase rounds
-#endif
-// per kernel (glm_engine's PF argument; each defaults to PFE_GLM_PF)
-#ifndef PFE_PF_GHIST
-#define PFE_PF_GHIST PFE_GLM_PF
-#endif
-#ifndef PFE_PF_GFIX
-#define PFE_PF_GFIX PFE_GLM_PF
-#endif
-#ifndef PFE_PF_GT1
-#define PFE_PF_GT1 PFE_GLM_PF
-#endif
-#ifndef PFE_PF_GDG
-#define PFE_PF_GDG PFE_GLM_PF
-#endif
-#ifndef PFE_PF_GDG8
-#define PFE_PF_GDG8 PFE_GLM_PF
-#endif
-#ifndef PFE_PF_SINE
-#define PFE_PF_SINE PFE_GLM_PF
-#endif
-#ifndef PFE_PF_DM
-#define PFE_PF_DM PFE_GLM_PF
-#endif
-#ifndef PFE_PF_PFDDM
-#define PFE_PF_PFDDM PFE_GLM_PF
-#endif
-template <int G, bool PF, class Prob, class Body>
-__device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Prob& prob,
-                                           const Body& body) {
+// Hand the slots of `mask` to the groups, NG = 64/G per round; body(f) runs in the group
+// that owns slot f (lanes of other groups are masked off).
+template <int G, class Body>
+__device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Body& body) {
   const int lane = lane_id();
   const int cnt = __builtin_popcountll(mask);
   if ((mask >> lane) & 1ull) list[__builtin_popcountll(mask & ((1ull << lane) - 1ull))] = lane;
   blm_sync();
   const int g = lane / G;
-  constexpr int NG = 64 / G;
-  if constexpr (PF) {
-    using Fn = std::decay_t<decltype(prob.load(0))>;
-    Fn fn;
-    if (g < cnt) fn = prob.load(list[g]);
-    for (int base = 0; base < cnt; base += NG) {
-      const int idx = base + g, nidx = idx + NG;
-      Fn nfn;
-      if (nidx < cnt) nfn = prob.load(list[nidx]);
-      if (idx < cnt) body(list[idx], fn);
-      fn = nfn;
-    }
-  } else {
-    for (int base = 0; base < cnt; base += NG) {
-      const int idx = base + g;
-      if (idx < cnt) body(list[idx], prob.load(list[idx]));
-    }
+  for (int base = 0; base < cnt; base += 64 / G) {
+    const int idx = base + g;
+    if (idx < cnt) body(list[idx]);
   }
   blm_sync();
 }
@@ -642,7 +580,7 @@ __device__ __forceinline__ void glm_rounds(uint64_t mask, int* list, const Prob&
 // ph / list: LDS int[FPW] each.  hand_region: hand-over scratch of FPW x hand_k x G doubles
 // per wave (block), or nullptr.  G: lanes per group (16 or 32; Prob::load lays the rows out
 // for the same G).
-template <int N, int MPL, int FPW, int G = GLM_G, int PF = PFE_GLM_PF, class Prob>
+template <int N, int MPL, int FPW, int G = GLM_G, class Prob>
 __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int* ph, int* list,
                                            double* hand_region = nullptr, int hand_k = 0) {
   static_assert(FPW <= 64, "one slot per lane in the SIMT phase");
@@ -683,7 +621,8 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // O-phase: fresh fits and accepted steps
     const uint64_t mo = __ballot(myph == PH_INIT || myph == PH_OUTER);
     if (mo) {
-      glm_rounds<G, (PF & 2) != 0>(mo, list, prob, [&](int f, const auto& fn) {
+      glm_rounds<G>(mo, list, [&](int f) {
+        const auto fn = prob.load(f);
         glm_outer<N, MPL, FPW, G>(fn, f, S, ph[f] == PH_INIT, hand);
       });
       if ((mo >> lane) & 1ull) ph[lane] = PH_LMPAR;
@@ -710,7 +649,8 @@ __device__ __forceinline__ void glm_engine(Prob& prob, BlmState<N, FPW>& S, int*
     // T-phase
     const uint64_t mt = __ballot(lane < FPW && ph[lane < FPW ? lane : 0] == PH_TRIAL);
     if (mt) {
-      glm_rounds<G, (PF & 1) != 0>(mt, list, prob, [&](int f, const auto& fn) {
+      glm_rounds<G>(mt, list, [&](int f) {
+        const auto fn = prob.load(f);
         const int nph = glm_trial<N, MPL, FPW, G>(fn, f, S, prob.maxfev(f), hand);
         if (glane<G>() == 0) ph[f] = nph;
       });

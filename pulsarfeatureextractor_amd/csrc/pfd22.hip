@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64, 2) void k_pfd_dmfitg(PfdDMArgs d) {
   if (lane_id() < FPW) T.cand[lane_id()] = -1;
   blm_sync();
   PfdDMProb<MPL, FPW> prob{d, T, term, used, d.a.gslots};
-  glm_engine<4, 4 * MPL, FPW, GLM_G, PFE_PF_PFDDM>(prob, S, T.ph, T.list, d.a.hand[HAND_DM], HAND_K_DM);
+  glm_engine<4, 4 * MPL, FPW>(prob, S, T.ph, T.list, d.a.hand[HAND_DM], HAND_K_DM);
 }
 
 size_t pfd22_workspace_bytes(int64_t n, int L) {
