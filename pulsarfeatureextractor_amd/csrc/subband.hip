@@ -596,7 +596,7 @@ void k_subband_fast(SubArgs a) {
       if (off < total) {
         const int band = off / LSB;
         uint16_t* row = E + band * STRIDE + 16 * pos;
-#ifndef PFE_SB_NOSWZ
+#if !defined(PFE_SB_NOSWZ) && !defined(PFE_SB_NOSWZ_ST)
         // a lane's 32 B go out as two 16-B stores; ds_write_b128 banks (dword mod 32) over 8
         // contiguous lanes, and lanes pos and pos + 4 (32 B apart) would hit the same 4 banks
         // if both stored their low half first: the upper four lanes of each eight store their
