@@ -480,3 +480,22 @@ def test_cli_gpus_flag_parses_devices(tmp_path, monkeypatch):
     assert cli.main(["-c", str(tmp_path / "c"), "-o", out, "--phcx", "--gpus", "2",
                      "--devices", "0,0"]) == 0
     assert seen["gpus"] == 2 and seen["devices"] == [0, 0] and seen["called"]
+
+
+class BrokenEngine(StubEngine):
+    def bates22(self, *a, **k):
+        raise RuntimeError("device lost")
+
+
+def test_sharded_run_reports_a_failing_worker(tmp_path, monkeypatch):
+    """A shard worker that raises fails the whole --gpus run with the worker's traceback and
+    merges nothing (the shard files stay for inspection; the progress marker is not moved)."""
+    monkeypatch.chdir(tmp_path)
+    d = make_dir(tmp_path)
+    out = str(tmp_path / "o.csv")
+    dp = processor.DataProcessor(engine=StubEngine(), workers=2, log=lambda *a: None, batch=8,
+                                 gpus=2, shard_engine="test_processor_host:BrokenEngine",
+                                 shard_slabs="test_processor_host:PlainSlabs")
+    with pytest.raises(RuntimeError, match="device lost"):
+        dp.processPHCXCollectively(d + "/", False, out, False, False, False)
+    assert not os.path.exists(out + ".progress")
