@@ -616,7 +616,7 @@ class RunMetrics:
                     self.score_s += dt
         return wrapped
 
-    def merge(self, m, rank, n, device):
+    def merge(self, m, rank, n, device, engine_start_s=None):
         """Fold one --gpus shard's metrics (its worker's finish()) into this run's: batches,
         failures by reason, the parser / GPU-stage timers summed over the workers (host
         seconds, as over the slots of one process), plus a per-shard entry."""
@@ -632,7 +632,7 @@ class RunMetrics:
                 if k.endswith("_s") and k[:-2] in ("pack", "gpu", "emit", "discover"):
                     self.stage[k[:-2]] = self.stage.get(k[:-2], 0.0) + v
             self.shards.append({"rank": rank, "device": int(device), "candidates": int(n),
-                                "wall_s": m.get("wall_s"),
+                                "engine_start_s": engine_start_s, "wall_s": m.get("wall_s"),
                                 "candidates_per_s": m.get("candidates_per_s")})
 
     def batch(self, res):
@@ -1187,9 +1187,7 @@ class DataProcessor:
         progress marker, so it resumes from --start as before."""
         import multiprocessing as mp
 
-        paths = list(paths)
-        n, g = len(paths), self.gpus
-        cuts = [n * r // g for r in range(g + 1)]
+        g = self.gpus
         devices = self.devices or _default_devices(g)
         threads = max(1, self.workers // g)
         ctx = mp.get_context("spawn")
@@ -1197,24 +1195,34 @@ class DataProcessor:
         kw = {"debugFlag": self.debug, "workers": threads, "batch": self.batch,
               "gpu_batch": self.gpu_batch, "gpu_depth": self.depth, "ramp": self.ramp}
         flags = {"phcx": self.phcx, "pfd": self.pfd, "superb": self.superb}
+        # the workers start (interpreter, engine, GPU) while the walk is still listing; each
+        # gets its shard of paths once the walk is done
         for r in range(g):
             sfx = f".shard{r}"
             a = list(args)
             if out_arg is not None:
                 a[out_arg] = a[out_arg] + sfx
-            rd, wr = ctx.Pipe(duplex=False)
+            mine, theirs = ctx.Pipe(duplex=True)
             p = ctx.Process(target=_shard_worker, name=f"pfe-shard{r}",
-                            args=(wr, kw, flags, entry, tuple(a), paths[cuts[r]:cuts[r + 1]], r,
-                                  sfx, int(devices[r % len(devices)]), self.shard_engine,
+                            args=(theirs, kw, flags, entry, tuple(a), r, sfx,
+                                  int(devices[r % len(devices)]), self.shard_engine,
                                   self.shard_slabs))
             p.start()
-            wr.close()
+            theirs.close()
             procs.append(p)
-            pipes.append(rd)
-        results, errors = [], []
-        for r, (p, rd) in enumerate(zip(procs, pipes)):
+            pipes.append(mine)
+        paths = list(paths)
+        n = len(paths)
+        cuts = [n * r // g for r in range(g + 1)]
+        for r, c in enumerate(pipes):
             try:
-                res = rd.recv()
+                c.send(paths[cuts[r]:cuts[r + 1]])
+            except (BrokenPipeError, OSError):
+                pass  # the worker failed while starting: its error is read below
+        results, errors = [], []
+        for r, (p, c) in enumerate(zip(procs, pipes)):
+            try:
+                res = c.recv()
             except EOFError:
                 res = {"error": f"shard {r}: worker exited with code {p.exitcode}"}
             p.join()
@@ -1248,7 +1256,8 @@ class DataProcessor:
         for r, res in enumerate(results):
             ok += res["ok"]
             failed += res["failed"]
-            run.merge(res.get("metrics"), r, cuts[r + 1] - cuts[r], devices[r % len(devices)])
+            run.merge(res.get("metrics"), r, cuts[r + 1] - cuts[r], devices[r % len(devices)],
+                      res.get("engine_start_s"))
         return ok, failed
 
     # ---- label mode (:691-826) --------------------------------------------------------
@@ -1359,12 +1368,17 @@ def _load_factory(spec):
 
 def _bind_numa(device):
     """Best effort: run this worker on the host CPUs of its GPU's NUMA node (sysfs), so its
-    reader threads and the first touch of its pinned slabs are node-local."""
+    reader threads and the first touch of its pinned slabs are node-local.  The PCI address
+    comes from the HIP runtime libpfe already loaded (no torch in a worker: its import and
+    device setup cost seconds per process)."""
     try:
-        import torch
+        import ctypes
 
-        pr = torch.cuda.get_device_properties(device)
-        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(device)) != 0:
+            return None
+        bus = buf.value.decode().lower()
         with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
             node = int(f.read().strip())
         if node < 0:
@@ -1384,12 +1398,14 @@ def _bind_numa(device):
     return None
 
 
-def _shard_worker(conn, kw, flags, entry, args, paths, rank, suffix, device, engine_spec,
+def _shard_worker(conn, kw, flags, entry, args, rank, suffix, device, engine_spec,
                   slabs_spec):
-    """One shard of a --gpus N run (a spawned process): a single-GPU DataProcessor on
-    `device` over `paths`, its files suffixed; sends {"ok", "failed", "metrics"} back."""
+    """One shard of a --gpus N run (a spawned process): opens its engine on `device`, then
+    receives its paths from the parent and runs a single-GPU DataProcessor over them, its files
+    suffixed; sends {"ok", "failed", "metrics"} back."""
     import traceback
 
+    t0 = time.perf_counter()
     try:
         if engine_spec:
             engine = _load_factory(engine_spec)()
@@ -1397,9 +1413,11 @@ def _shard_worker(conn, kw, flags, entry, args, paths, rank, suffix, device, eng
             from .candidate import set_engine
             from ._native import Engine
 
-            _bind_numa(device)
             engine = Engine(device)
+            _bind_numa(device)
             set_engine(engine)
+        init_s = time.perf_counter() - t0  # interpreter imports done: the engine's start
+        paths = conn.recv()
         dp = DataProcessor(engine=engine, log=lambda *a: print(f"[shard {rank}]", *a), **kw)
         if slabs_spec:
             dp._slabs = _load_factory(slabs_spec)()
@@ -1417,7 +1435,7 @@ def _shard_worker(conn, kw, flags, entry, args, paths, rank, suffix, device, eng
         dp._summary = capture
         getattr(dp, entry)(*args)
         conn.send({"ok": counts.get("ok", 0), "failed": counts.get("failed", 0),
-                   "metrics": dp.metrics})
+                   "metrics": dp.metrics, "engine_start_s": init_s})
     except BaseException:  # noqa: BLE001 -- reported to the parent
         conn.send({"error": f"shard {rank}:\n" + traceback.format_exc()})
     finally:
