@@ -1348,14 +1348,32 @@ def _as_matrix(res):
     return mat, skip
 
 
-def _default_devices(g):
-    """rank r -> GPU r % (visible GPUs); counting devices does not initialise the GPU."""
+def _visible_gpus():
+    """GPUs this process may use, without initialising one (and without importing torch,
+    whose first import costs seconds): the HIP / ROCr / CUDA visibility list when one is
+    set, else the GPU nodes of the KFD topology (nodes with SIMDs)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip():
+            return len([x for x in v.split(",") if x.strip()])
+    n = 0
     try:
-        import torch
+        base = "/sys/class/kfd/kfd/topology/nodes"
+        for node in os.listdir(base):
+            with open(os.path.join(base, node, "properties")) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+                        break
+    except (OSError, ValueError):
+        return 0
+    return n
 
-        nd = torch.cuda.device_count()
-    except Exception:  # noqa: BLE001
-        nd = 0
+
+def _default_devices(g):
+    """rank r -> GPU r % (visible GPUs)."""
+    nd = _visible_gpus()
     return list(range(max(1, min(g, nd)))) if nd else [0]
 
 
