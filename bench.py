@@ -445,9 +445,10 @@ def run_lyon8(ctx, args, n, lp):
     elapsed, kern_ms, kern_max = ctx.time_steps(step, args.steps, args.warmup)
     bytes_per_launch = n * (lp + args.ld + 8 * 8)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    # HBM bytes per launch: the round-4 PMC passes of this command at the current defaults
+    # HBM bytes per launch: the latest round's PMC passes of this command at the current defaults
     # (tools/gpu_steps.sh trace_l8 pmc_l8 -> tools/summarize_prof.py); round 2's if absent
-    traffic = (load_traffic(f"r05_lyon8_u8_{lp}x{args.ld}_n{n}.json")
+    traffic = (load_traffic(f"r06_lyon8_u8_{lp}x{args.ld}_n{n}.json")
+               or load_traffic(f"r05_lyon8_u8_{lp}x{args.ld}_n{n}.json")
                or load_traffic(f"r04_lyon8_u8_{lp}x{args.ld}_n{n}.json")
                or load_traffic(f"lyon8_u8_{lp}x{args.ld}_n{n}_pmc.json"))
     return {
