@@ -101,10 +101,12 @@ constexpr int BLM_FPW = 32;  // most fits per wave in the batched kernels (LDS s
 constexpr int GLM_FPW = 32;  // fit slots per wave of the pooled group-LM kernels (lm_group.h)
 static_assert(GLM_FPW == BLM_FPW, "per-wave scratch is sized by BLM_FPW");
 // fit slots per wave of k_gdg8g: its SIMT phase (lmpar, one slot per lane) is the largest
-// share of the 8-parameter kernel, which runs one wave per SIMD (registers), so 48 slots
-// fill more lanes there; the LDS state (BlmState<8, 48>, 35 KB) still admits 4 waves per CU
+// share of the 8-parameter kernel, which runs one wave per SIMD (registers), so as many slots
+// as the LDS admits at 4 waves per CU: BlmState<8, 53> + slot table = 40 928 B of 40 960
+// (round 6: 48 -> 53 slots, k_gdg8g 273.5 -> 271.3 ms per 1M, every output bit-identical,
+// profiles/r06_ab_slots53.txt)
 #ifndef PFE_GDG8_FPW
-#define PFE_GDG8_FPW 48
+#define PFE_GDG8_FPW 53
 #endif
 constexpr int GDG8_FPW = PFE_GDG8_FPW;
 // waves per SIMD k_gdg8g is compiled for (its registers: 1)
