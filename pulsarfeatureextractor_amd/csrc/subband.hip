@@ -34,6 +34,7 @@
 #include <cmath>
 
 #include "../../include/pfe.h"
+#include <type_traits>
 #include "bates_common.h"
 #include "wave.h"
 
@@ -643,6 +644,12 @@ void k_subband_fast(SubArgs a) {
   double W[SL];
 #pragma unroll
   for (int k = 0; k < SL; ++k) W[k] = 0.0;
+  uint32_t zh[SL];  // held zeros: the high halves of pass 2's denormal byte-sum operands
+#pragma unroll
+  for (int k = 0; k < SL; ++k) {
+    zh[k] = 0u;
+    asm volatile("" : "+v"(zh[k]));
+  }
   double C = 0.0;
   int valid = 0;
   // pass 2's window slots (lane = window): the prefix indices, band-independent (a window
@@ -680,24 +687,47 @@ void k_subband_fast(SubArgs a) {
     const uint16_t* phi = plo + wb;
     int sv = 0, kl = 0;
     unsigned long long qv = 0;
+    // sum b^2 in 64 bits; for windows of <= 64 bins (b <= 255 * 64) sixteen squares fit 32
+    // bits, so they are summed in a 32-bit register and widened once per 16 steps (a 32-bit
+    // add issues at about half the cost of the 64-bit one, profiles/r05_ubench_op_rates.txt)
+    auto pass1 = [&](auto narrow_c) {
+      constexpr bool NAR = decltype(narrow_c)::value;
+      uint32_t q32 = 0;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      if (4 * ch < U) {  // wave-uniform
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (4 * ch < U) {  // wave-uniform
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int u = 4 * ch + v;
-          const int o = 8 * (u >> 1) + (u & 1);
-          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
-          // the lane's own key: ties go to the smaller step (the smaller j of this lane)
-          const int kk = (int)((b << 6) | (uint32_t)(63 - u));
-          kl = kk > kl ? kk : kl;
-          sv += (int)b;
-          // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
-          // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
-          qv += (uint32_t)__umul24(b, b);
+          for (int v = 0; v < 4; ++v) {
+            const int u = 4 * ch + v;
+            const int o = 8 * (u >> 1) + (u & 1);
+            const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
+            // the lane's own key: ties go to the smaller step (the smaller j of this lane)
+            const int kk = (int)((b << 6) | (uint32_t)(63 - u));
+            kl = kk > kl ? kk : kl;
+            sv += (int)b;
+            // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
+            // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
+            if constexpr (NAR)
+              q32 += (uint32_t)__umul24(b, b);
+            else
+              qv += (uint32_t)__umul24(b, b);
+          }
+          if constexpr (NAR) {
+            if (ch % 4 == 3) {
+              qv += q32;
+              q32 = 0;
+            }
+          }
         }
       }
-    }
+      if constexpr (NAR) qv += q32;
+    };
+#ifndef PFE_SB_NOQ32
+    if (wb <= 64)
+      pass1(std::true_type{});
+    else
+#endif
+      pass1(std::false_type{});
     // the lane's best window as the band-wide key (b << 10) | (1023 - j), then the band's four
     // quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums and a maximum
     const int ub = 63 - (kl & 63);
@@ -717,10 +747,22 @@ void k_subband_fast(SubArgs a) {
     valid += __builtin_popcountll(__ballot(lane < 16 && ok));
     // ---- pass 2: W_j += r_i b_ij in band order (the 16 bands' r and S r through LDS,
     // broadcast reads; C summed in band order) ---------------------------------------------
+#ifndef PFE_SB_NODENORM
+    // the boxcar sum b (an integer < 2^17) enters the fma as the denormal b * 2^-1074: its
+    // 32 bits in the low half of a register pair whose high half is a held zero (no
+    // conversion instruction), against r * 2^1022, so every product and partial sum is
+    // numpy's times 2^-52 exactly (all terms are >= 0 and >= 2^-79 when non-zero: no
+    // subnormal rounding) and W is scaled back once at the end
+    if (lane < 16) {
+      fold[bi] = rl * 0x1p1022;
+      fold[16 + bi] = cl;
+    }
+#else
     if (lane < 16) {
       fold[bi] = rl;
       fold[16 + bi] = cl;
     }
+#endif
     wave_lds_sync();
 #pragma unroll
     for (int ii = 0; ii < SB_NB; ii += 2) {
@@ -730,15 +772,30 @@ void k_subband_fast(SubArgs a) {
       C += c2.y;
       const uint16_t* row0 = rows + ii * STRIDE;
       const uint16_t* row1 = row0 + STRIDE;
+#ifndef PFE_SB_NODENORM
+#pragma unroll
+      for (int k = 0; k < SL; ++k)
+        W[k] = __builtin_fma(r2.x, __builtin_bit_cast(double, ((uint64_t)zh[k] << 32) |
+                             (uint32_t)((int)row0[hi_k[k]] - (int)row0[lo_k[k]])), W[k]);
+#pragma unroll
+      for (int k = 0; k < SL; ++k)
+        W[k] = __builtin_fma(r2.y, __builtin_bit_cast(double, ((uint64_t)zh[k] << 32) |
+                             (uint32_t)((int)row1[hi_k[k]] - (int)row1[lo_k[k]])), W[k]);
+#else
 #pragma unroll
       for (int k = 0; k < SL; ++k)
         W[k] = __builtin_fma(r2.x, (double)((int)row0[hi_k[k]] - (int)row0[lo_k[k]]), W[k]);
 #pragma unroll
       for (int k = 0; k < SL; ++k)
         W[k] = __builtin_fma(r2.y, (double)((int)row1[hi_k[k]] - (int)row1[lo_k[k]]), W[k]);
+#endif
     }
     wave_lds_sync();
   }
+#ifndef PFE_SB_NODENORM
+#pragma unroll
+  for (int k = 0; k < SL; ++k) W[k] *= 0x1p52;  // exact
+#endif
   // s21: sum_{i<k} cc_ik = (sum_j Z_j^2 - v) / 2 with Z_j = nw W_j - C, |z_i|^2 = 1
   double zs = 0.0;
 #pragma unroll
