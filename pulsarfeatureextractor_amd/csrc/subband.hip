@@ -687,47 +687,24 @@ void k_subband_fast(SubArgs a) {
     const uint16_t* phi = plo + wb;
     int sv = 0, kl = 0;
     unsigned long long qv = 0;
-    // sum b^2 in 64 bits; for windows of <= 64 bins (b <= 255 * 64) sixteen squares fit 32
-    // bits, so they are summed in a 32-bit register and widened once per 16 steps (a 32-bit
-    // add issues at about half the cost of the 64-bit one, profiles/r05_ubench_op_rates.txt)
-    auto pass1 = [&](auto narrow_c) {
-      constexpr bool NAR = decltype(narrow_c)::value;
-      uint32_t q32 = 0;
 #pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        if (4 * ch < U) {  // wave-uniform
+    for (int ch = 0; ch < NCH; ++ch) {
+      if (4 * ch < U) {  // wave-uniform
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int u = 4 * ch + v;
-            const int o = 8 * (u >> 1) + (u & 1);
-            const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
-            // the lane's own key: ties go to the smaller step (the smaller j of this lane)
-            const int kk = (int)((b << 6) | (uint32_t)(63 - u));
-            kl = kk > kl ? kk : kl;
-            sv += (int)b;
-            // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
-            // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
-            if constexpr (NAR)
-              q32 += (uint32_t)__umul24(b, b);
-            else
-              qv += (uint32_t)__umul24(b, b);
-          }
-          if constexpr (NAR) {
-            if (ch % 4 == 3) {
-              qv += q32;
-              q32 = 0;
-            }
-          }
+        for (int v = 0; v < 4; ++v) {
+          const int u = 4 * ch + v;
+          const int o = 8 * (u >> 1) + (u & 1);
+          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
+          // the lane's own key: ties go to the smaller step (the smaller j of this lane)
+          const int kk = (int)((b << 6) | (uint32_t)(63 - u));
+          kl = kk > kl ? kk : kl;
+          sv += (int)b;
+          // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
+          // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
+          qv += (uint32_t)__umul24(b, b);
         }
       }
-      if constexpr (NAR) qv += q32;
-    };
-#ifndef PFE_SB_NOQ32
-    if (wb <= 64)
-      pass1(std::true_type{});
-    else
-#endif
-      pass1(std::false_type{});
+    }
     // the lane's best window as the band-wide key (b << 10) | (1023 - j), then the band's four
     // quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums and a maximum
     const int ub = 63 - (kl & 63);
