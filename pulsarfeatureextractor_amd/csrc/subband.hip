@@ -34,7 +34,6 @@
 #include <cmath>
 
 #include "../../include/pfe.h"
-#include <type_traits>
 #include "bates_common.h"
 #include "wave.h"
 
