@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "../../include/pfe.h"
 #include "bates_common.h"
@@ -52,6 +53,8 @@ struct SubArgs {
 };
 
 constexpr int SB_NB = 16;  // bands per register block
+constexpr int SB_PK_WB = 32;  // widest boxcar of the fast kernel's packed pass 1
+typedef unsigned short us2v __attribute__((ext_vector_type(2)));
 
 // LDS row stride (elements) of the prefix array: 16-B aligned rows of lsb + 1 entries
 template <typename PT>
@@ -684,30 +687,92 @@ void k_subband_fast(SubArgs a) {
     // ---- pass 1: S = sum b, sum b^2 and the first maximum of each band -------------------
     const uint16_t* plo = rows + bi * STRIDE + 2 * qtr;
     const uint16_t* phi = plo + wb;
-    int sv = 0, kl = 0;
+    int sv = 0, key = 0;
     unsigned long long qv = 0;
+#ifndef PFE_SB_NOPK
+    if (wb <= SB_PK_WB) {
+      // packed: the lane's two windows of a step pair s, j = 8s + 2 qtr + {0, 1}, as the u16
+      // halves of one register: (E[j], E[j + 1]) is an aligned dword (j even), and so is
+      // (E[j + wb], E[j + 1 + wb]) for an even wb (an odd one takes the two dwords around it,
+      // joined by one v_alignbit).  Per pair: one saturating v_pk_sub_u16 (b of both windows),
+      // two v_dot2_u32_u16 (S, sum b^2) and a v_lshl_or + v_pk_max_u16 for the maxima -- 5
+      // VALU for two windows instead of 7 for one.  Exact while wb <= 32: b <= 255 wb < 2^13,
+      // so (b << 3) | step fits a half, and a lane's <= 64 squares stay below 2^32.
+      int sq = 0;
+      const uint32_t* dlo = reinterpret_cast<const uint32_t*>(plo);
+      const uint32_t* dhi = reinterpret_cast<const uint32_t*>(plo + (wb & ~1));
+      const int S2 = (U >> 1);  // step pairs (ceil(nw / 8))
+      auto pairs = [&](auto odd_c) {
+        constexpr bool ODD = decltype(odd_c)::value;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      if (4 * ch < U) {  // wave-uniform
+        for (int g = 0; g < (NCH + 1) / 2; ++g) {  // chunks of 8 pairs: 3 bits of step index
+          if (8 * g < S2) {                        // wave-uniform
+            uint32_t km = 0;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int u = 4 * ch + v;
-          const int o = 8 * (u >> 1) + (u & 1);
-          const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
-          // the lane's own key: ties go to the smaller step (the smaller j of this lane)
-          const int kk = (int)((b << 6) | (uint32_t)(63 - u));
-          kl = kk > kl ? kk : kl;
-          sv += (int)b;
-          // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
-          // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
-          qv += (uint32_t)__umul24(b, b);
+            for (int t = 0; t < 8; t += 2) {
+              if (t > 0 && 8 * g + t >= S2) break;  // wave-uniform, two pairs at a time
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int sp = 8 * g + t + e;
+                const uint32_t lo = dlo[4 * sp];
+                const uint32_t hi = ODD ? __builtin_amdgcn_alignbit(dhi[4 * sp + 1], dhi[4 * sp], 16)
+                                        : dhi[4 * sp];
+                const us2v b2 = __builtin_elementwise_sub_sat(__builtin_bit_cast(us2v, hi),
+                                                              __builtin_bit_cast(us2v, lo));
+                sv = (int)__builtin_amdgcn_udot2(b2, (us2v){1, 1}, (uint32_t)sv, false);
+                sq = (int)__builtin_amdgcn_udot2(b2, b2, (uint32_t)sq, false);
+                // both halves' keys (b << 3) | (7 - step): ties go to the smaller step
+                const uint32_t k2 = (__builtin_bit_cast(uint32_t, b2) << 3) |
+                                    (uint32_t)((7 - t - e) * 0x10001);
+                km = __builtin_bit_cast(uint32_t,
+                                        __builtin_elementwise_max(__builtin_bit_cast(us2v, k2),
+                                                                  __builtin_bit_cast(us2v, km)));
+              }
+            }
+            // the chunk's two half maxima as band-wide keys (b << 10) | (1023 - j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t kh = (km >> (16 * h)) & 0xFFFFu;
+              const int j = 8 * (8 * g + 7 - (int)(kh & 7u)) + 2 * qtr + h;
+              const int kk = (int)((kh >> 3) << 10) | (1023 - j);
+              key = kk > key ? kk : key;
+            }
+          }
+        }
+      };
+      if (wb & 1)  // wave-uniform
+        pairs(std::true_type{});
+      else
+        pairs(std::false_type{});
+      qv = (uint32_t)sq;
+    } else
+#endif
+    {
+      int kl = 0;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (4 * ch < U) {  // wave-uniform
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int u = 4 * ch + v;
+            const int o = 8 * (u >> 1) + (u & 1);
+            const uint32_t b = __builtin_elementwise_sub_sat((uint32_t)phi[o], (uint32_t)plo[o]);
+            // the lane's own key: ties go to the smaller step (the smaller j of this lane)
+            const int kk = (int)((b << 6) | (uint32_t)(63 - u));
+            kl = kk > kl ? kk : kl;
+            sv += (int)b;
+            // b < 2^16: the 24-bit multiply is exact; HIP declares __umul24 as returning int,
+            // so the cast keeps a product >= 2^31 (b >= 46 341) from being sign-extended
+            qv += (uint32_t)__umul24(b, b);
+          }
         }
       }
+      // the lane's best window as the band-wide key (b << 10) | (1023 - j)
+      const int ub = 63 - (kl & 63);
+      key = ((kl >> 6) << 10) | (1023 - (8 * (ub >> 1) + 2 * qtr + (ub & 1)));
     }
-    // the lane's best window as the band-wide key (b << 10) | (1023 - j), then the band's four
-    // quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums and a maximum
-    const int ub = 63 - (kl & 63);
-    int key = ((kl >> 6) << 10) | (1023 - (8 * (ub >> 1) + 2 * qtr + (ub & 1)));
+    // the band's four quarter lanes (bi, bi + 16, bi + 32, bi + 48) combined: integer sums
+    // and a maximum
     sv += __shfl_xor(sv, 16);
     qv += xor_u64<16>(qv);
     key = max(key, __shfl_xor(key, 16));

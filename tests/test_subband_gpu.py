@@ -101,6 +101,33 @@ def test_subband3_bright_wide_windows(engine, nsub, lsb):
     check(out, st, ref, ok, f"bright {nsub}x{lsb}", lsb)
 
 
+@pytest.mark.parametrize("nsub,lsb", [(16, 256), (20, 128), (16, 64), (3, 32)])
+def test_subband3_packed_pass_boundary(engine, nsub, lsb):
+    """The fast kernel's packed pass 1 (two windows per register, wb <= 32) at its bounds:
+    windows of 29-36 bins (both parities, both sides of 32) and 1-3 bins, saturated bands
+    (every byte 255: b = 255 wb, the largest the packed keys and 32-bit square sums hold),
+    random bright bands and ties between equal windows."""
+    wbs = [w for w in (1, 2, 3, 29, 30, 31, 32, 33, 34, 36) if w <= lsb]
+    n = 4 * len(wbs)
+    b = bates_batch(n, lp=lsb, nsub=nsub, lsb=lsb, seed=1300 + lsb)
+    rng = np.random.default_rng(1400 + lsb)
+    for i in range(n):
+        b["scal"][i, 3] = wbs[i % len(wbs)] / lsb  # exact: ceil(w * lsb) = wb
+        kind = i // len(wbs)
+        if kind == 0:
+            b["sub"][i] = 255
+            b["sub"][i, :, 0] = rng.integers(0, 256, size=nsub)  # keep the bands varying
+        elif kind == 1:
+            b["sub"][i] = rng.integers(200, 256, size=b["sub"][i].shape, dtype=np.uint8)
+        elif kind == 2:
+            b["sub"][i] = 0
+            b["sub"][i, :, ::8] = 255                              # periodic: tied windows
+            b["sub"][i, :, 1] = rng.integers(0, 256, size=nsub)
+    out, st = engine.subband3(b["prof"], b["sub"], b["scal"])
+    ref, ok = oracle_sub(b["prof"], b["sub"], b["scal"])
+    check(out, st, ref, ok, f"packed {nsub}x{lsb}", lsb)
+
+
 def test_subband3_matches_bates22_columns_and_device(engine):
     import torch
 

@@ -39,6 +39,13 @@ def dump(path):
             out, st = e.subband3(b["prof"], b["sub"], b["scal"])
             res[f"sub{nsub}x{lsb}_out"] = np.asarray(out)
             res[f"sub{nsub}x{lsb}_st"] = np.asarray(st)
+            # the same bands with wide windows (wb up to 60 % of the band) and bright rows
+            rng = np.random.default_rng(seed)
+            b["scal"][:, 3] = rng.uniform(0.5 / lsb, 0.6, size=n)
+            b["sub"][: n // 4] = np.maximum(b["sub"][: n // 4], 200)
+            out, st = e.subband3(b["prof"], b["sub"], b["scal"])
+            res[f"sub{nsub}x{lsb}w_out"] = np.asarray(out)
+            res[f"sub{nsub}x{lsb}w_st"] = np.asarray(st)
         # pfe_pfd_dmprof (fast sweep: L = 64/128 with nsub % 8 == 0; the others general) and
         # pfe_pfd_bates22
         from bench import pfd_block
