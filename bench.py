@@ -613,12 +613,13 @@ def run_subband(ctx, args, n, lsb, steps, warmup):
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": load_traffic(f"r06_subband_16x{lsb}_n{n}.json"),
             "kernel": f"pfe::k_subband_fast<{lsb}, 4>",
             "algorithmic_bytes_per_candidate": per_cand,
             "note": "bytes-based roofline for comparability; the kernel is VALU-issue bound "
-                    "(1.88k VALU wave instructions per candidate measured, profiles/r04_subband_sq_counters.json; 3 waves/SIMD at 166 VGPRs), "
-                    "see DESIGN.md section 3.3",
+                    "(1.26k VALU wave instructions per candidate measured, profiles/r06_subband_sq_counters.json; "
+                    "86 VGPRs, 10 KiB of LDS per wave), see DESIGN.md section 3.3",
             "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
         },
     }, out

@@ -19,6 +19,7 @@
 #   sq_l8dm      two SQ counter passes over the nDM = 120 kernel + tools/sq_summary.py
 #   sq_sub       two SQ counter passes over the config-4 sub-band kernel (bench.py --path subband)
 #   trace_sub    kernel trace of bench.py --path subband
+#   pmc_sub      FETCH_SIZE and WRITE_SIZE passes of the same command (one pass each)
 #   e2e          tools/e2e_bench.py --mode stream on 50 000 synthetic PHCX files
 #   golden_dump  the 22 scores of every golden set (tools/golden_dump.py; host: envelope_report)
 #   pfdab        bench.py --path pfd with the split pipeline (default) and fused (pfd_split=0)
@@ -109,6 +110,12 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_trsub -o tr -- \
         python3 bench.py --path subband --steps 10 --warmup 2 --no-cpu-baseline --no-extra \
         > $O/${T}_trsub.json 2> $O/${T}_trsub.err || fail trace_sub $O/${T}_trsub.err ;;
+    pmc_sub)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/${T}_pmc_sub_$c -o pmc -- \
+          python3 bench.py --path subband --steps 5 --warmup 1 --no-cpu-baseline --no-extra \
+          > $O/${T}_pmc_sub_$c.log 2>&1 || fail pmc_sub $O/${T}_pmc_sub_$c.log
+      done ;;
     e2e)
       timeout -k 10 600 python -u tools/e2e_bench.py --mode stream --n 50000 --dir /tmp/pfe_e2e \
         --depth ${E2E_DEPTH:-1,2} ${E2E_OPT} > $O/${T}_e2e.json 2> $O/${T}_e2e.err || fail e2e $O/${T}_e2e.err ;;

@@ -29,7 +29,11 @@ def main():
     ap.add_argument("--tag", required=True)
     ap.add_argument("--out", default="profiles")
     a = ap.parse_args()
-    stats = [r for r in rows(os.path.join(a.trace, "trace_kernel_stats.csv"))]
+    import glob
+    ks = sorted(glob.glob(os.path.join(a.trace, "**", "*kernel_stats.csv"), recursive=True))
+    if not ks:
+        raise SystemExit(f"no *kernel_stats.csv under {a.trace}")
+    stats = [r for r in rows(ks[0])]
     k = [r for r in stats if a.kernel in r["Name"]]
     if not k:
         raise SystemExit("kernel not found in stats")
