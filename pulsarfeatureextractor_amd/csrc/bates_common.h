@@ -212,4 +212,56 @@ __device__ __forceinline__ FMeanStd f_mean_std(const double (&v)[MPL], const boo
 // Python's builtin min(a, b): returns a unless b < a
 __device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
 
+// ---- the DM-curve models' per-row arithmetic, bit-exact and cheaper -------------------------
+// a / B for a constant B, correctly rounded: with Y = RN(1/B), q = RN(a Y), r = fma(-q, B, a)
+// (exact) and fma(r, Y, q) = RN(a / B) by Markstein's theorem whenever nothing under- or
+// overflows (|a| in [2^-900, 2^900]; tests/test_recipdiv.py checks both divisors), three
+// instructions instead of an IEEE division's ~11; a row outside that range (0, inf, NaN, a
+// diverging fit) takes the division -- a wave branch around it, so the common case carries
+// none of the division's instructions.
+#ifndef PFE_DM_DIVF3
+#define PFE_DM_DIVF3 1
+#endif
+template <int64_t B>
+__device__ __forceinline__ double div_const(double a) {
+#if PFE_DM_DIVF3
+  constexpr double D = (double)B, Y = 1.0 / (double)B;
+  const double q = a * Y;
+  double t = __builtin_fma(__builtin_fma(-q, D, a), Y, q);
+  const double aa = __builtin_fabs(a);
+  const bool ok = aa >= 0x1p-900 && aa <= 0x1p900;
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) t = ok ? t : a / D;
+  return t;
+#else
+  return a / (double)B;
+#endif
+}
+
+// sqrt(x), correctly rounded: the compiler's own gfx950 expansion (v_rsq_f64, then two
+// Goldschmidt / Newton steps by fma) without its pre-scaling of x < 2^-767 by 2^256 and its
+// +-0 / +inf fix-up, so the same bits for every x in [2^-767, inf) in 10 instructions instead
+// of 18; a wave with any other x (0, inf, NaN, negative, tiny) takes sqrt() for those rows.
+#ifndef PFE_DM_SQRT
+#define PFE_DM_SQRT 1
+#endif
+__device__ __forceinline__ double sqrt_rn(double x) {
+#if PFE_DM_SQRT
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  h = __builtin_fma(h, r, h);
+  g = __builtin_fma(g, r, g);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  const bool ok = x >= 0x1p-767 && x < __builtin_inf();
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) g = ok ? g : __builtin_sqrt(x);
+  return g;
+#else
+  return __builtin_sqrt(x);
+#endif
+}
+
 }  // namespace pfe

@@ -428,28 +428,8 @@ constexpr double KDM = 8.3 * 1000000.0;   // 8.3*10**6 (PHCXOperations.py:187)
 constexpr double DF = 400.0;
 constexpr double F3 = 2593941624.0;       // pow(1374, 3), an exact integer
 
-// a / F3 correctly rounded: with Y = RN(1/F3), q = RN(a Y), r = fma(-q, F3, a) (exact) and
-// fma(r, Y, q) = RN(a / F3) by Markstein's theorem whenever nothing under- or overflows
-// (|a| in [2^-900, 2^900]; tests/test_recipdiv.py checks it for this divisor), three
-// instructions instead of an IEEE division's ~11 in every row of every DM-model evaluation;
-// a row outside that range (0, inf, NaN, or a diverging fit) takes the division -- a wave
-// branch around it, so the common case carries none of the division's instructions.
-#ifndef PFE_DM_DIVF3
-#define PFE_DM_DIVF3 1
-#endif
-__device__ __forceinline__ double div_f3(double a) {
-#if PFE_DM_DIVF3
-  constexpr double Y = 1.0 / F3;
-  const double q = a * Y;
-  double t = __builtin_fma(__builtin_fma(-q, F3, a), Y, q);
-  const double aa = __builtin_fabs(a);
-  const bool ok = aa >= 0x1p-900 && aa <= 0x1p900;
-  if (__builtin_expect(__ballot(!ok) != 0, 0)) t = ok ? t : a / F3;
-  return t;
-#else
-  return a / F3;
-#endif
-}
+static_assert(F3 == 2593941624.0, "div_f3 is this divisor");
+__device__ __forceinline__ double div_f3(double a) { return div_const<2593941624LL>(a); }
 
 template <int MPL>
 struct DMFn {
@@ -462,8 +442,8 @@ struct DMFn {
   double wint, dm, period;
   __device__ __forceinline__ double shape(const double (&p)[3], int k) const {
     const double t = div_f3(p[1] * KDM * fabs((dm + p[2]) - x[k]) * DF);   // :152
-    const double weff = sqrt(wint + t * t);
-    return sqrt((period - weff) / weff);
+    const double weff = sqrt_rn(wint + t * t);
+    return sqrt_rn((period - weff) / weff);
   }
   __device__ __forceinline__ double model(const double (&p)[3], int k) const {
     return p[0] * shape(p, k);                                         // :153

@@ -30,6 +30,7 @@ hipError_t fork_end(const Fork* fk, hipStream_t st);
 constexpr double KDM_PFD = 8.3 * 1000000.0;  // 8.3*10**6      (PFDOperations.py:342)
 constexpr double DF_PFD = 32.0;              // df = 32         (:343)
 constexpr double F3_PFD = 2460375.0;         // pow(135, 3), an exact integer (:344)
+static_assert(F3_PFD == 2460375.0, "div_const<2460375> in PfdDMFn::weff is this divisor");
 
 // residuals of getDMFittings (:302-310): y - (Up + Amp*sqrt((P - w)/w)), w clamped to P
 template <int MPL>
@@ -38,14 +39,14 @@ struct PfdDMFn {
   bool ok[MPL];
   double wint, dm, period;
   __device__ __forceinline__ double weff(double prop, double shift, int k) const {
-    const double t = prop * KDM_PFD * fabs((dm + shift) - x[k]) * DF_PFD / F3_PFD;
-    double w = sqrt(wint + t * t);
+    const double t = div_const<2460375LL>(prop * KDM_PFD * fabs((dm + shift) - x[k]) * DF_PFD);
+    double w = sqrt_rn(wint + t * t);
     if (w > period) w = period;                                        // :305-307
     return w;
   }
   __device__ __forceinline__ double model(const double (&p)[4], int k) const {
     const double w = weff(p[1], p[2], k);
-    return p[3] + p[0] * sqrt((period - w) / w);                       // :308
+    return p[3] + p[0] * sqrt_rn((period - w) / w);                    // :308
   }
   __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll

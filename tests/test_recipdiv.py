@@ -30,8 +30,8 @@ int main(int argc, char** argv) {
     double b = mk(-500, 499, mode == 1);
     double a = mk(-900, 400, mode == 2);
     if (mode == 3) { b = mk(-3, 3, 0); a = mk(-2, 8, 0); }   /* the fits' usual range */
-    if (argc > 2) {  /* the DM model's constant divisor F3 = 1374^3 (div_f3) */
-      b = 2593941624.0;
+    if (argc > 2) {  /* the DM models' constant divisors (div_const): 1374^3, 135^3 */
+      b = strtod(argv[2], 0);
       a = (i & 1) ? mk(-900, 900, 0) : mk(20, 40, 0);
     }
     volatile double y = 1.0 / b;
@@ -61,8 +61,10 @@ def test_shared_divisor_quotient_is_correctly_rounded():
         assert out.returncode == 0, out.stdout
         n, bad = map(int, out.stdout.split()[-2:])
         assert n == 4000000 and bad == 0
-        # div_f3 of the DM-curve model (bates_sine_dm_sub.hip): b = F3, |a| in [2^-900, 2^900]
-        out = subprocess.run([exe, "4000000", "f3"], capture_output=True, text=True, timeout=120)
-        assert out.returncode == 0, out.stdout
-        n, bad = map(int, out.stdout.split()[-2:])
-        assert n == 4000000 and bad == 0
+        # div_const of the DM-curve models (bates_common.h): PHCX F3 = 1374^3, PFD 135^3,
+        # |a| in [2^-900, 2^900]
+        for f3 in ("2593941624", "2460375"):
+            out = subprocess.run([exe, "4000000", f3], capture_output=True, text=True, timeout=120)
+            assert out.returncode == 0, out.stdout
+            n, bad = map(int, out.stdout.split()[-2:])
+            assert n == 4000000 and bad == 0
