@@ -19,6 +19,15 @@ LIB = os.path.join(LIBDIR, "libpfe.so")
 SOURCES = ["capi.hip", "lyon8.hip", "bates22.hip", "bates_sine_dm_sub.hip", "bates_gauss.hip", "bates_gauss_peel.hip",
            "bates_gauss_dg8.hip", "subband.hip",
            "pfd.hip", "pfd22.hip"]
+# The Levenberg-Marquardt translation units are compiled without the two-address v_fmac_f64:
+# with it the register allocator copies the accumulator (a v_mov_b64 per fma whose addend
+# stays live -- every polynomial coefficient of exp, every Householder update), ~600 extra
+# VALU per k_gdgg; the three-address v_fma_f64 needs none.  Same operations, same bits
+# (tools/ab.sh exact), k_gdgg / k_gdg8g 3-4 % faster (profiles/r06_ab_no_fmac.txt).  The
+# host half of hipcc ignores the feature with a warning.
+NO_FMAC = ["-Xclang", "-target-feature", "-Xclang", "-fmacf64-inst"]
+NO_FMAC_SOURCES = {"bates_sine_dm_sub.hip", "bates_gauss.hip", "bates_gauss_peel.hip",
+                   "bates_gauss_dg8.hip", "pfd22.hip"}
 HOST_SOURCES = ["phcx_io.cpp"]  # host-only C++ (PHCX reader / batch packer), built with g++
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]
 ARCH = os.environ.get("PFE_OFFLOAD_ARCH", "gfx950")
@@ -53,16 +62,19 @@ def _needs(obj: str, deps: list[str]) -> bool:
 
 
 def build(verbose: bool = False, force: bool = False, variant: str = "",
-          defines: tuple[str, ...] = (), csrc: str | None = None) -> str:
+          defines: tuple[str, ...] = (), csrc: str | None = None,
+          flags: tuple[str, ...] = ()) -> str:
     """Compile every source and link lib/libpfe.so.  A non-empty ``variant`` builds an
     instrumented copy (lib/libpfe_<variant>.so, objects under lib/obj_<variant>/) with the
     extra -D ``defines`` (e.g. the LM phase-cycle profiler, -DPFE_LM_PROFILE); the product
     library is never built with them.  ``csrc``: another source tree for a variant (an A/B
-    against an earlier revision: tools/build_variant.py)."""
+    against an earlier revision: tools/build_variant.py); ``flags``: extra compiler arguments of
+    a variant's kernels."""
     CSRC = csrc or globals()["CSRC"]
     builddir = BUILDDIR + (f"_{variant}" if variant else "")
     lib = os.path.join(LIBDIR, f"libpfe_{variant}.so") if variant else LIB
     extra = [f"-D{d}" for d in defines]
+    kflags = list(flags)
     os.makedirs(builddir, exist_ok=True)
     cc = hipcc()
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
@@ -74,7 +86,8 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
         o = os.path.join(builddir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _needs(o, [s] + headers):
-            jobs.append([cc, *COMMON, *extra, "-c", s, "-o", o])
+            tu = NO_FMAC if src in NO_FMAC_SOURCES else []
+            jobs.append([cc, *COMMON, *tu, *extra, *kflags, "-c", s, "-o", o])
 
     cxx = shutil.which("g++") or "g++"
     for src in HOST_SOURCES:

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Build an A/B variant of libpfe.so (host side, in the build container).
 
-  tools/build_variant.py NAME [--rev REV] [-D DEF ...]
+  tools/build_variant.py NAME [--rev REV] [-D DEF ...] [--flag=ARG ...]
 
 -> pulsarfeatureextractor_amd/lib/libpfe_NAME.so, from the kernel sources (csrc/ and
-include/) of git revision REV (default: the working tree) with the extra -D definitions.
+include/) of git revision REV (default: the working tree) with the extra -D definitions and
+compiler arguments (--flag=-Xclang, one argument each).
 The variant's objects go to lib/obj_NAME/; the product library is not touched.  Run the A/B
 on the GPU box with tools/ab.sh.
 """
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--rev", default=None)
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--flag", dest="flags", action="append", default=[])
     a = ap.parse_args()
     from pulsarfeatureextractor_amd import build as b
 
@@ -50,7 +52,7 @@ def main():
         csrc = export(a.rev, tmp)
     try:
         print(b.build(verbose=False, force=True, variant=a.name, defines=tuple(a.defines),
-                      csrc=csrc))
+                      csrc=csrc, flags=tuple(a.flags)))
     finally:
         if tmp:
             shutil.rmtree(tmp, ignore_errors=True)
