@@ -46,6 +46,37 @@ struct PlainDiv {
   double b;
   __device__ __forceinline__ double operator()(double a) const { return a / b; }
 };
+// exp(-(t*t) / 2), the Gaussian models' only exponential, with the device library's own
+// algorithm (ocml exp_f64: n = rint(x log2 e), the two-part reduction, its degree-12
+// polynomial, ldexp) minus its x > 1024 -> +inf select, which an argument <= 0 (or NaN) never
+// takes: the same bits, two instructions fewer per row and evaluation.
+#ifndef PFE_GAUSS_EXP
+#define PFE_GAUSS_EXP 1
+#endif
+__device__ __forceinline__ double exp_neg_half_sq(double t) {
+  const double x = -(t * t) / 2.0;
+#if PFE_GAUSS_EXP
+  const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
+  double f = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, x);
+  f = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, f);
+  double p = __builtin_fma(f, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+  p = __builtin_fma(f, p, 0x1.71dee623fde64p-19);
+  p = __builtin_fma(f, p, 0x1.a01997c89e6b0p-16);
+  p = __builtin_fma(f, p, 0x1.a01a014761f6ep-13);
+  p = __builtin_fma(f, p, 0x1.6c16c1852b7b0p-10);
+  p = __builtin_fma(f, p, 0x1.1111111122322p-7);
+  p = __builtin_fma(f, p, 0x1.55555555502a1p-5);
+  p = __builtin_fma(f, p, 0x1.5555555555511p-3);
+  p = __builtin_fma(f, p, 0x1.000000000000bp-1);
+  p = __builtin_fma(f, p, 1.0);
+  p = __builtin_fma(f, p, 1.0);
+  const double e = __builtin_ldexp(p, (int)dn);
+  return x < -1075.0 ? 0.0 : e;
+#else
+  return exp(x);
+#endif
+}
+
 template <class Body>
 __device__ __forceinline__ void with_div(double sigma, double mu, const Body& body) {
   const double as = fabs(sigma);
@@ -213,7 +244,7 @@ struct GaussFn {  // y - |A| exp(-((x-mu)/sigma)^2 / 2)
   template <class D>
   __device__ __forceinline__ double model(const D& dv, const double (&p)[3], int k) const {
     const double t = dv(x[k] - p[1]);
-    return fabs(p[2]) * exp(-(t * t) / 2.0);
+    return fabs(p[2]) * exp_neg_half_sq(t);
   }
   __device__ __forceinline__ double model(const double (&p)[3], int k) const {
     return model(PlainDiv{p[0]}, p, k);
@@ -234,7 +265,7 @@ struct GaussFixedFn {  // mu fixed at xmax; parameters (sigma, A)
   template <class D>
   __device__ __forceinline__ double model(const D& dv, const double (&p)[2], int k) const {
     const double t = dv(x[k] - xmax);
-    return fabs(p[1]) * exp(-(t * t) / 2.0);
+    return fabs(p[1]) * exp_neg_half_sq(t);
   }
   __device__ __forceinline__ double model(const double (&p)[2], int k) const {
     return model(PlainDiv{p[0]}, p, k);
@@ -618,7 +649,7 @@ struct GaussFnWide {  // y - |A| exp(-((x-mu)/sigma)^2 / 2) over the rows of a W
   template <class D>
   __device__ __forceinline__ double model(const D& dv, const double (&p)[3], double xv) const {
     const double t = dv(xv - p[1]);
-    return fabs(p[2]) * exp(-(t * t) / 2.0);
+    return fabs(p[2]) * exp_neg_half_sq(t);
   }
   __device__ __forceinline__ void operator()(const double (&p)[3], double* f) const {
     const int lane = lane_id();
@@ -643,7 +674,7 @@ struct GaussFixedFnWide {  // mu fixed at xmax; parameters (sigma, A)
         double v = 0.0;
         if (i < w.m) {
           const double t = dv(w.x(i) - xmax);
-          v = w.y(i) - fabs(p[1]) * exp(-(t * t) / 2.0);
+          v = w.y(i) - fabs(p[1]) * exp_neg_half_sq(t);
         }
         f[k * 64 + lane] = v;
       }
@@ -1152,7 +1183,7 @@ struct GaussBgFn {  // y - (|A| exp(-((x-mu)/|sigma|)^2/2) + bg)      (:1226)
   template <class D>
   __device__ __forceinline__ double term(const D& dv, const double (&p)[4], int k) const {
     const double t = dv(x[k] - p[1]);
-    return exp(-(t * t) / 2.0);
+    return exp_neg_half_sq(t);
   }
   __device__ __forceinline__ double model(const double (&p)[4], int k) const {
     return fabs(p[2]) * term(PlainDiv{fabs(p[0])}, p, k) + p[3];
@@ -1338,7 +1369,7 @@ struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
   template <class D>
   __device__ __forceinline__ double term(const D& dv, const double (&p)[4], int k) const {
     const double t = dv(x[k] - p[1]);
-    return exp(-(t * t) / 2.0);
+    return exp_neg_half_sq(t);
   }
   __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
     with_div(p[0], p[1], [&](const auto& dv) {
@@ -1373,7 +1404,7 @@ struct GaussAbsBgFn {  // y - (|A| exp(-((x-mu)/sigma)^2/2) + |bg|)     (:1296)
 };
 __device__ __forceinline__ double g_absbg(double x, const double (&p)[4]) {
   const double t = (x - p[1]) / p[0];
-  return fabs(p[2]) * exp(-(t * t) / 2.0) + fabs(p[3]);
+  return fabs(p[2]) * exp_neg_half_sq(t) + fabs(p[3]);
 }
 
 template <int MPL>
@@ -1387,12 +1418,12 @@ struct DoubleGaussFn {  // :1459-1460
   template <class D>
   __device__ __forceinline__ double term1(const D& dv, const double (&p)[8], int k) const {
     const double t1 = dv(x[k] - p[1]);
-    return exp(-(t1 * t1) / 2.0);
+    return exp_neg_half_sq(t1);
   }
   template <class D>
   __device__ __forceinline__ double term2(const D& dv, const double (&p)[8], int k) const {
     const double t2 = dv(x[k] - p[5]);
-    return exp(-(t2 * t2) / 2.0);
+    return exp_neg_half_sq(t2);
   }
   __device__ __forceinline__ double term1(const double (&p)[8], int k) const {
     return term1(PlainDiv{fabs(p[0])}, p, k);
@@ -1880,7 +1911,7 @@ __device__ __forceinline__ void gdg8_finish(const BatesArgs& a, int64_t c, const
   for (int k = 0; k < P; ++k) {
     const double x = dg.x[k];
     const double tt = (x - t1p[1]) / fabs(t1p[0]);
-    const double gf = fabs(t1p[2]) * exp(-(tt * tt) / 2.0) + t1p[3];
+    const double gf = fabs(t1p[2]) * exp_neg_half_sq(tt) + t1p[3];
     dd[k] = (use_final ? ffit[k] : cfit[k]) - (gf + w.minbg - w.pstd);
     if (ok[k]) s += dd[k];
   }
