@@ -237,31 +237,10 @@ __device__ __forceinline__ double div_const(double a) {
 #endif
 }
 
-// sqrt(x), correctly rounded: the compiler's own gfx950 expansion (v_rsq_f64, then two
-// Goldschmidt / Newton steps by fma) without its pre-scaling of x < 2^-767 by 2^256 and its
-// +-0 / +inf fix-up, so the same bits for every x in [2^-767, inf) in 10 instructions instead
-// of 18; a wave with any other x (0, inf, NaN, negative, tiny) takes sqrt() for those rows.
+// the DM models' square roots: sqrt_rn (wave.h) unless PFE_DM_SQRT=0
 #ifndef PFE_DM_SQRT
 #define PFE_DM_SQRT 1
 #endif
-__device__ __forceinline__ double sqrt_rn(double x) {
-#if PFE_DM_SQRT
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y;
-  double h = y * 0.5;
-  const double r = __builtin_fma(-h, g, 0.5);
-  h = __builtin_fma(h, r, h);
-  g = __builtin_fma(g, r, g);
-  double d = __builtin_fma(-g, g, x);
-  g = __builtin_fma(d, h, g);
-  d = __builtin_fma(-g, g, x);
-  g = __builtin_fma(d, h, g);
-  const bool ok = x >= 0x1p-767 && x < __builtin_inf();
-  if (__builtin_expect(__ballot(!ok) != 0, 0)) g = ok ? g : __builtin_sqrt(x);
-  return g;
-#else
-  return __builtin_sqrt(x);
-#endif
-}
+__device__ __forceinline__ double dm_sqrt(double x) { return PFE_DM_SQRT ? sqrt_rn(x) : sqrt(x); }
 
 }  // namespace pfe

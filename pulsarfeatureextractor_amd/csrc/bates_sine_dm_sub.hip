@@ -442,8 +442,8 @@ struct DMFn {
   double wint, dm, period;
   __device__ __forceinline__ double shape(const double (&p)[3], int k) const {
     const double t = div_f3(p[1] * KDM * fabs((dm + p[2]) - x[k]) * DF);   // :152
-    const double weff = sqrt_rn(wint + t * t);
-    return sqrt_rn((period - weff) / weff);
+    const double weff = dm_sqrt(wint + t * t);
+    return dm_sqrt((period - weff) / weff);
   }
   __device__ __forceinline__ double model(const double (&p)[3], int k) const {
     return p[0] * shape(p, k);                                         // :153

@@ -40,13 +40,13 @@ struct PfdDMFn {
   double wint, dm, period;
   __device__ __forceinline__ double weff(double prop, double shift, int k) const {
     const double t = div_const<2460375LL>(prop * KDM_PFD * fabs((dm + shift) - x[k]) * DF_PFD);
-    double w = sqrt_rn(wint + t * t);
+    double w = dm_sqrt(wint + t * t);
     if (w > period) w = period;                                        // :305-307
     return w;
   }
   __device__ __forceinline__ double model(const double (&p)[4], int k) const {
     const double w = weff(p[1], p[2], k);
-    return p[3] + p[0] * sqrt_rn((period - w) / w);                    // :308
+    return p[3] + p[0] * dm_sqrt((period - w) / w);                    // :308
   }
   __device__ __forceinline__ void operator()(const double (&p)[4], double (&f)[MPL]) const {
 #pragma unroll

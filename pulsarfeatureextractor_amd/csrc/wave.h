@@ -148,4 +148,25 @@ __device__ __forceinline__ void put(T (&a)[N], int idx, T v) {
   for (int k = 0; k < N; ++k) a[k] = (idx == k) ? v : opaque(a[k]);
 }
 
+// sqrt(x), correctly rounded: the compiler's own gfx950 expansion (v_rsq_f64, then two
+// Goldschmidt / Newton steps by fma) without its pre-scaling of x < 2^-767 by 2^256 and its
+// +-0 / +inf fix-up, so the same bits for every x in [2^-767, inf) in 10 instructions instead
+// of 18; a wave with any other x (0, inf, NaN, negative, tiny) takes sqrt() for those lanes
+// (a ballot over the active lanes, so it may sit in divergent code).
+__device__ __forceinline__ double sqrt_rn(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  h = __builtin_fma(h, r, h);
+  g = __builtin_fma(g, r, g);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  const bool ok = x >= 0x1p-767 && x < __builtin_inf();
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) g = ok ? g : __builtin_sqrt(x);
+  return g;
+}
+
 }  // namespace pfe
