@@ -618,7 +618,7 @@ def run_subband(ctx, args, n, lsb, steps, warmup):
             "kernel": f"pfe::k_subband_fast<{lsb}, 4>",
             "algorithmic_bytes_per_candidate": per_cand,
             "note": "bytes-based roofline for comparability; the kernel is VALU-issue bound "
-                    "(1.26k VALU wave instructions per candidate measured, profiles/r06_subband_sq_counters.json; "
+                    "(1.22k VALU wave instructions per candidate measured, profiles/r06_ab_subband_sdwa.txt; "
                     "86 VGPRs, 10 KiB of LDS per wave), see DESIGN.md section 3.3",
             "avg_kernel_ms": kern_ms, "avg_kernel_ms_max_over_ranks": kern_max,
         },

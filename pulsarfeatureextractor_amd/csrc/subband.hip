@@ -576,6 +576,31 @@ void k_subband_fast(SubArgs a) {
       for (int d = 0; d < 4; ++d) tot = __builtin_amdgcn_sad_u8(wv[d], 0u, tot);
       uint32_t e = seg_scan_incl<SEG>(tot, pos) - tot;
       uint32_t pk[8];
+#ifndef PFE_SB_NOSDWA
+      // the chain straight into the packed u16 pairs, one SDWA add per prefix: WORD_1 of a
+      // pair = its WORD_0 + the next byte (the low half kept), WORD_0 of the next pair = the
+      // previous WORD_1 + the byte after (the high half zeroed) -- 16 adds per 16 bytes, no
+      // shifts or ors (every prefix is < 2^16 at <= 256 bins, so a half holds it exactly)
+      const uint32_t excl = e;
+      {
+        uint32_t c = e;  // WORD_0 = the running prefix, WORD_1 = 0
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t x = wv[d];
+          uint32_t n;
+          asm("v_add_u32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:BYTE_0"
+              : "+v"(c) : "v"(x));
+          asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_1"
+              : "=v"(n) : "v"(c), "v"(x));
+          asm("v_add_u32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:BYTE_2"
+              : "+v"(n) : "v"(x));
+          pk[2 * d] = c;
+          pk[2 * d + 1] = n;
+          asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_3"
+              : "=v"(c) : "v"(n), "v"(x));
+        }
+      }
+#else
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t x = wv[d];
@@ -588,6 +613,7 @@ void k_subband_fast(SubArgs a) {
         pk[2 * d + 1] = e2 | (e3 << 16);
       }
       const uint32_t excl = e - tot;
+#endif
       int X2 = 0, XP = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
