@@ -20,7 +20,13 @@ import os
 
 
 def py2_str(x) -> str:
-    """Python 2.7 str() of a float (12 significant digits)."""
+    """Python 2.7 str() of a float (12 significant digits).
+
+    Pinned by CPython 2.7's definition rather than by Python-2-written files (none ship with
+    the reference, and no Python 2 is available here): float_str is
+    PyOS_double_to_string(v, 'g', 12, Py_DTSF_ADD_DOT_0) -- correctly rounded '%.12g' with
+    ".0" appended when the text has neither a point nor an exponent; tests/test_writers.py
+    holds the edge cases (integral values, -0.0, 12/13-digit integers, 1e-05, subnormals)."""
     x = float(x)
     if math.isnan(x):
         return "nan"

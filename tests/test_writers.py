@@ -10,7 +10,8 @@ def test_py2_str_cases():
     cases = {0.1: "0.1", 1.0 / 3: "0.333333333333", 1e20: "1e+20", 100.0: "100.0",
              -0.0: "-0.0", 123456789.123456789: "123456789.123", 1e-5: "1e-05",
              2.5e-300: "2.5e-300", 12345678901.0: "12345678901.0",
-             123456789012.0: "123456789012.0", 1234567890123.0: "1.23456789012e+12"}
+             123456789012.0: "123456789012.0", 1234567890123.0: "1.23456789012e+12",
+             5e-324: "4.94065645841e-324", 1e16: "1e+16", 0.0001: "0.0001"}
     for v, s in cases.items():
         assert writers.py2_str(v) == s, (v, writers.py2_str(v), s)
 
