@@ -728,18 +728,21 @@ void k_subband_fast(SubArgs a) {
       const uint32_t* dlo = reinterpret_cast<const uint32_t*>(plo);
       const uint32_t* dhi = reinterpret_cast<const uint32_t*>(plo + (wb & ~1));
       const int S2 = (U >> 1);  // step pairs (ceil(nw / 8))
-      auto pairs = [&](auto odd_c) {
+      // IB bits of step index per key half: chunks of 2^IB step pairs, folded to the band key
+      // once per chunk; b < 2^(16 - IB), so IB = 4 (half the folds) for wb <= 16
+      auto pairs = [&](auto odd_c, auto ib_c) {
         constexpr bool ODD = decltype(odd_c)::value;
+        constexpr int IB = decltype(ib_c)::value, CP = 1 << IB;
 #pragma unroll
-        for (int g = 0; g < (NCH + 1) / 2; ++g) {  // chunks of 8 pairs: 3 bits of step index
-          if (8 * g < S2) {                        // wave-uniform
+        for (int g = 0; g < (2 * NCH + CP - 1) / CP; ++g) {
+          if (CP * g < S2) {  // wave-uniform
             uint32_t km = 0;
 #pragma unroll
-            for (int t = 0; t < 8; t += 2) {
-              if (t > 0 && 8 * g + t >= S2) break;  // wave-uniform, two pairs at a time
+            for (int t = 0; t < CP; t += 2) {
+              if (t > 0 && CP * g + t >= S2) break;  // wave-uniform, two pairs at a time
 #pragma unroll
               for (int e = 0; e < 2; ++e) {
-                const int sp = 8 * g + t + e;
+                const int sp = CP * g + t + e;
                 const uint32_t lo = dlo[4 * sp];
                 const uint32_t hi = ODD ? __builtin_amdgcn_alignbit(dhi[4 * sp + 1], dhi[4 * sp], 16)
                                         : dhi[4 * sp];
@@ -747,9 +750,9 @@ void k_subband_fast(SubArgs a) {
                                                               __builtin_bit_cast(us2v, lo));
                 sv = (int)__builtin_amdgcn_udot2(b2, (us2v){1, 1}, (uint32_t)sv, false);
                 sq = (int)__builtin_amdgcn_udot2(b2, b2, (uint32_t)sq, false);
-                // both halves' keys (b << 3) | (7 - step): ties go to the smaller step
-                const uint32_t k2 = (__builtin_bit_cast(uint32_t, b2) << 3) |
-                                    (uint32_t)((7 - t - e) * 0x10001);
+                // both halves' keys (b << IB) | (CP - 1 - step): ties go to the smaller step
+                const uint32_t k2 = (__builtin_bit_cast(uint32_t, b2) << IB) |
+                                    (uint32_t)((CP - 1 - t - e) * 0x10001);
                 km = __builtin_bit_cast(uint32_t,
                                         __builtin_elementwise_max(__builtin_bit_cast(us2v, k2),
                                                                   __builtin_bit_cast(us2v, km)));
@@ -759,17 +762,26 @@ void k_subband_fast(SubArgs a) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const uint32_t kh = (km >> (16 * h)) & 0xFFFFu;
-              const int j = 8 * (8 * g + 7 - (int)(kh & 7u)) + 2 * qtr + h;
-              const int kk = (int)((kh >> 3) << 10) | (1023 - j);
+              const int j = 8 * (CP * g + CP - 1 - (int)(kh & (CP - 1u))) + 2 * qtr + h;
+              const int kk = (int)((kh >> IB) << 10) | (1023 - j);
               key = kk > key ? kk : key;
             }
           }
         }
       };
-      if (wb & 1)  // wave-uniform
-        pairs(std::true_type{});
-      else
-        pairs(std::false_type{});
+      using I3 = std::integral_constant<int, 3>;
+      using I4 = std::integral_constant<int, 4>;
+      if (wb <= 16) {  // wave-uniform
+        if (wb & 1)
+          pairs(std::true_type{}, I4{});
+        else
+          pairs(std::false_type{}, I4{});
+      } else {
+        if (wb & 1)
+          pairs(std::true_type{}, I3{});
+        else
+          pairs(std::false_type{}, I3{});
+      }
       qv = (uint32_t)sq;
     } else
 #endif

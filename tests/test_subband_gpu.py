@@ -103,11 +103,12 @@ def test_subband3_bright_wide_windows(engine, nsub, lsb):
 
 @pytest.mark.parametrize("nsub,lsb", [(16, 256), (20, 128), (16, 64), (3, 32)])
 def test_subband3_packed_pass_boundary(engine, nsub, lsb):
-    """The fast kernel's packed pass 1 (two windows per register, wb <= 32) at its bounds:
+    """The fast kernel's packed pass 1 (two windows per register, wb <= 32; 16-pair chunks
+    for wb <= 16) at its bounds:
     windows of 29-36 bins (both parities, both sides of 32) and 1-3 bins, saturated bands
     (every byte 255: b = 255 wb, the largest the packed keys and 32-bit square sums hold),
     random bright bands and ties between equal windows."""
-    wbs = [w for w in (1, 2, 3, 29, 30, 31, 32, 33, 34, 36) if w <= lsb]
+    wbs = [w for w in (1, 2, 3, 15, 16, 17, 29, 30, 31, 32, 33, 34, 36) if w <= lsb]
     n = 4 * len(wbs)
     b = bates_batch(n, lp=lsb, nsub=nsub, lsb=lsb, seed=1300 + lsb)
     rng = np.random.default_rng(1400 + lsb)
